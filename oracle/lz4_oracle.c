@@ -1,0 +1,362 @@
+/*
+ * oracle/lz4_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the LZ4 r1.3.0 block codec vendored by KingDB
+ * (/root/reference/algorithm/lz4.{h,cc}) and of KingDB's CompressorLZ4 frame
+ * wrapper (/root/reference/algorithm/compressor.cc), plus CRC32C and the
+ * synthetic data generators the benchmark configs name.
+ *
+ * It exists only as the CHECKER: tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product (kingdb_amd/) never
+ * links, loads or calls anything in this directory; the product path runs the
+ * HIP kernels in kingdb_amd/csrc and fails loudly if they are unavailable.
+ *
+ * Parity of this restatement is PINNED against the reference itself: the
+ * recipe in oracle/Makefile compiles the reference's own lz4.cc/compressor.cc
+ * from /root/reference into oracle/_ref/ (never copied into the repo), and
+ * tests/golden/make_golden.py uses that build to emit the committed golden
+ * fixtures and to cross-check this file on randomized inputs.
+ *
+ * Style note: this is written index-based (positions, not pointers) so that it
+ * reads like the GPU kernels' specification; every rule cites the reference
+ * line it restates.  All arithmetic is integer/byte.
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <string.h>
+
+/* ---- constants: lz4.cc:222-246, lz4.h:60,102-103 ---------------------- */
+#define ORC_MINMATCH      4            /* lz4.cc:226 */
+#define ORC_LASTLITERALS  5            /* lz4.cc:229 */
+#define ORC_MFLIMIT       12           /* lz4.cc:230  (COPYLENGTH+MINMATCH) */
+#define ORC_MINLENGTH     13           /* lz4.cc:231  (MFLIMIT+1) */
+#define ORC_64KLIMIT      (65536 + 11) /* lz4.cc:237 */
+#define ORC_SKIPSTRENGTH  6            /* lz4.cc:238 */
+#define ORC_MAX_DISTANCE  65535        /* lz4.cc:241 */
+#define ORC_ML_MASK       15u          /* lz4.cc:244 */
+#define ORC_RUN_MASK      15u          /* lz4.cc:246 */
+#define ORC_MAX_INPUT     0x7E000000u  /* lz4.h:102 */
+#define ORC_HASHLOG       12           /* LZ4_MEMORY_USAGE(14) - 2, lz4.cc:222 */
+
+static inline uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* lz4.h:103 / lz4.cc:371 */
+int orc_compress_bound(int isize) {
+  if ((unsigned)isize > ORC_MAX_INPUT) return 0;
+  return isize + isize / 255 + 16;
+}
+
+/* lz4.cc:373-379: byU16 uses a 13-bit hash (>>19), byU32 a 12-bit one (>>20). */
+static inline uint32_t hash_at(const uint8_t* src, uint32_t pos, int wide) {
+  uint32_t v = rd32(src + pos) * 2654435761u;
+  return wide ? (v >> (32 - ORC_HASHLOG)) : (v >> (32 - ORC_HASHLOG - 1));
+}
+
+/* lz4.cc:412-428: common prefix length of [a..) and [b..), never reaching
+ * `limit` (an absolute position).  The 8/4/2/1-byte stepping of the reference
+ * is equivalent to min(LCP, limit - a). */
+static uint32_t common_len(const uint8_t* src, uint32_t a, uint32_t b, uint32_t limit) {
+  uint32_t n = 0;
+  while (a + n < limit && src[a + n] == src[b + n]) n++;
+  return n;
+}
+
+/*
+ * LZ4_compress_limitedOutput (lz4.cc:664-682) instantiating
+ * LZ4_compress_generic(limitedOutput, byU16|byU32, noDict, noDictIssue)
+ * (lz4.cc:431-641).  Returns bytes written, or 0 when the output does not fit
+ * in max_out (checked exactly where the reference checks).
+ *
+ * NOTE: like the reference, a run of zero-literal sequences is not checked
+ * against max_out (lz4.cc:626-628 re-enters _next_match with no test), so with
+ * a max_out below the bound the encoder may write past max_out before a later
+ * check returns 0.  Callers give `dst` room for orc_compress_bound(isize) + 8
+ * bytes; the return value (0 or the size) is what is specified.
+ *
+ * The table holds positions; it is zero-initialised (lz4.cc:669), so an empty
+ * slot reads back as position 0.
+ */
+int orc_compress_limited(const uint8_t* src, uint8_t* dst, int isize, int max_out) {
+  uint32_t table[8192];
+  memset(table, 0, sizeof(table));                              /* lz4.cc:669 */
+  if ((uint32_t)isize > ORC_MAX_INPUT) return 0;                /* lz4.cc:465 */
+  const int wide = isize >= ORC_64KLIMIT;                       /* lz4.cc:673-676 */
+  const uint32_t n = (uint32_t)isize;
+  const int64_t olimit = max_out;
+  int64_t op = 0;                       /* next output byte */
+  uint32_t anchor = 0;                  /* first pending literal */
+  uint32_t ip = 0;
+
+  if (n >= ORC_MINLENGTH) {                                     /* lz4.cc:483 */
+    const uint32_t mflimit = n - ORC_MFLIMIT;
+    const uint32_t matchlimit = n - ORC_LASTLITERALS;
+    uint32_t fwd_h;
+    table[hash_at(src, 0, wide)] = 0;                           /* lz4.cc:486 */
+    ip = 1;
+    fwd_h = hash_at(src, ip, wide);                             /* lz4.cc:487 */
+
+    for (;;) {
+      uint32_t ref;
+      int64_t token;
+      /* ---- search loop, lz4.cc:494-527 ---- */
+      {
+        uint32_t fwd_ip = ip;
+        uint32_t step = 1;
+        uint32_t nb = 1u << ORC_SKIPSTRENGTH;
+        for (;;) {
+          uint32_t h = fwd_h;
+          ip = fwd_ip;
+          fwd_ip += step;
+          step = (nb++) >> ORC_SKIPSTRENGTH;
+          if (fwd_ip > mflimit) goto last_literals;            /* lz4.cc:510 */
+          ref = table[h];                                       /* lz4.cc:512 */
+          fwd_h = hash_at(src, fwd_ip, wide);                   /* lz4.cc:525 */
+          table[h] = ip;                                        /* lz4.cc:526 */
+          if (wide && ref + ORC_MAX_DISTANCE < ip) continue;    /* lz4.cc:530 (byU32 only) */
+          if (rd32(src + ref) == rd32(src + ip)) break;         /* lz4.cc:531 */
+        }
+      }
+      /* ---- catch up, lz4.cc:535 ---- */
+      while (ip > anchor && ref > 0 && src[ip - 1] == src[ref - 1]) { ip--; ref--; }
+
+      /* ---- literal length + literals, lz4.cc:537-554 ---- */
+      {
+        uint32_t lit = ip - anchor;
+        token = op++;
+        if (op + lit + (2 + 1 + ORC_LASTLITERALS) + lit / 255 > olimit) return 0;
+        if (lit >= ORC_RUN_MASK) {
+          int64_t len = (int64_t)lit - ORC_RUN_MASK;
+          dst[token] = (uint8_t)(ORC_RUN_MASK << 4);
+          for (; len >= 255; len -= 255) dst[op++] = 255;
+          dst[op++] = (uint8_t)len;
+        } else {
+          dst[token] = (uint8_t)(lit << 4);
+        }
+        memcpy(dst + op, src + anchor, lit);
+        op += lit;
+      }
+
+    next_match:
+      /* ---- offset, lz4.cc:558 ---- */
+      {
+        uint32_t off = ip - ref;
+        dst[op++] = (uint8_t)off;
+        dst[op++] = (uint8_t)(off >> 8);
+      }
+      /* ---- match length, lz4.cc:562-596 ---- */
+      {
+        uint32_t ml = common_len(src, ip + ORC_MINMATCH, ref + ORC_MINMATCH, matchlimit);
+        ip += ORC_MINMATCH + ml;
+        if (ml >= ORC_ML_MASK) {
+          if (op + (1 + ORC_LASTLITERALS) + (ml >> 8) > olimit) return 0;
+          dst[token] += ORC_ML_MASK;
+          ml -= ORC_ML_MASK;
+          for (; ml >= 510; ml -= 510) { dst[op++] = 255; dst[op++] = 255; }
+          if (ml >= 255) { ml -= 255; dst[op++] = 255; }
+          dst[op++] = (uint8_t)ml;
+        } else {
+          dst[token] += (uint8_t)ml;
+        }
+      }
+      anchor = ip;
+      if (ip > mflimit) break;                                  /* lz4.cc:601 */
+
+      /* ---- fill table + test next position, lz4.cc:604-628 ---- */
+      table[hash_at(src, ip - 2, wide)] = ip - 2;
+      {
+        uint32_t h = hash_at(src, ip, wide);
+        ref = table[h];
+        table[h] = ip;
+        if (ref + ORC_MAX_DISTANCE >= ip && rd32(src + ref) == rd32(src + ip)) {
+          token = op++;
+          dst[token] = 0;
+          goto next_match;
+        }
+      }
+      fwd_h = hash_at(src, ++ip, wide);                         /* lz4.cc:631 */
+    }
+  }
+
+last_literals:
+  /* ---- last literals, lz4.cc:634-645 ---- */
+  {
+    int64_t run = (int64_t)n - anchor;
+    if (op + run + 1 + (run + 255 - ORC_RUN_MASK) / 255 > (int64_t)(uint32_t)max_out) return 0;
+    if (run >= (int64_t)ORC_RUN_MASK) {
+      int64_t r = run - ORC_RUN_MASK;
+      dst[op++] = (uint8_t)(ORC_RUN_MASK << 4);
+      for (; r >= 255; r -= 255) dst[op++] = 255;
+      dst[op++] = (uint8_t)r;
+    } else {
+      dst[op++] = (uint8_t)(run << 4);
+    }
+    memcpy(dst + op, src + anchor, (size_t)run);
+    op += run;
+  }
+  return (int)op;
+}
+
+/*
+ * LZ4_decompress_safe_partial (lz4.cc:1050-1053) =
+ * LZ4_decompress_generic(endOnInputSize, partial, target, noDict) (lz4.cc:876-1042).
+ *
+ * Returns bytes decoded, or -(consumed)-1 on malformed input, with `consumed`
+ * the input cursor at the point the reference detects the error.
+ *
+ * Out-of-range input bytes: the reference reads the token and the first
+ * literal-length byte without checking ip < iend (lz4.cc:917, 924).  Those are
+ * the only reads that can leave [src, src+csize); this restatement (and the
+ * GPU kernel) define such a byte as 0, and the golden fixtures are generated
+ * with zero padding after every block so the reference sees the same value.
+ */
+int orc_decompress_safe_partial(const uint8_t* src, uint8_t* dst, int csize,
+                                int target, int max_out) {
+  const int64_t iend = csize;
+  const int64_t oend = max_out;
+  int64_t ip = 0, op = 0;
+  int64_t oexit = target;
+  if (oexit > oend - ORC_MFLIMIT) oexit = oend - ORC_MFLIMIT;          /* lz4.cc:910 */
+  if (max_out == 0) return (csize == 1 && src[0] == 0) ? 0 : -1;      /* lz4.cc:911 */
+#define IN(i) ((i) >= 0 && (i) < iend ? src[(i)] : 0)
+
+  for (;;) {
+    uint32_t token = IN(ip); ip++;
+    int64_t length = token >> 4;
+    if (length == ORC_RUN_MASK) {                                      /* lz4.cc:920-927 */
+      uint32_t s;
+      do { s = IN(ip); ip++; length += s; } while (ip < iend - ORC_RUN_MASK && s == 255);
+    }
+    /* literals, lz4.cc:932-956 */
+    {
+      int64_t cpy = op + length;
+      if (cpy > oexit || ip + length > iend - (2 + 1 + ORC_LASTLITERALS)) {
+        if (cpy > oend) goto fail;
+        if (ip + length > iend) goto fail;
+        memcpy(dst + op, src + ip, (size_t)length);
+        ip += length;
+        op += length;
+        break;
+      }
+      memcpy(dst + op, src + ip, (size_t)length);
+      ip += length;
+      op = cpy;
+    }
+    /* offset, lz4.cc:959-960 (checkOffset: dictSize 0 < 64K) */
+    int64_t ref = op - (int64_t)(IN(ip) | (IN(ip + 1) << 8));
+    ip += 2;
+    if (ref < 0) goto fail;
+    /* match length, lz4.cc:963-973 */
+    length = token & ORC_ML_MASK;
+    if (length == ORC_ML_MASK) {
+      uint32_t s;
+      do {
+        if (ip > iend - ORC_LASTLITERALS) goto fail;
+        s = IN(ip); ip++;
+        length += s;
+      } while (s == 255);
+    }
+    /* copy, lz4.cc:1005-1030: the end-of-block rule is "match end must stay
+     * <= oend-5"; the dec32/dec64 overlap trick equals a forward byte copy. */
+    {
+      int64_t mend = op + length + ORC_MINMATCH;
+      if (mend > oend - 12 && mend > oend - ORC_LASTLITERALS) goto fail;
+      /* The reference also writes op..op+7 before that test (lz4.cc:1008-1018);
+       * those bytes lie inside [0, oend) and are rewritten later, so the
+       * observable result on success is the forward byte copy below. */
+      for (int64_t i = 0; i < length + ORC_MINMATCH; i++) dst[op + i] = dst[ref + i];
+      op = mend;
+    }
+  }
+  return (int)op;
+fail:
+  return (int)(-ip - 1);
+#undef IN
+}
+
+/* ---- CRC32C (Castagnoli, reflected 0x82F63B78): crc32c.cc:296-340 ------- */
+static uint32_t crc_table[256];
+static int crc_init_done = 0;
+static void crc_init(void) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    crc_table[i] = c;
+  }
+  crc_init_done = 1;
+}
+uint32_t orc_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n) {
+  if (!crc_init_done) crc_init();
+  uint32_t l = crc ^ 0xffffffffu;
+  for (size_t i = 0; i < n; i++) l = crc_table[(l ^ p[i]) & 0xff] ^ (l >> 8);
+  return l ^ 0xffffffffu;
+}
+
+/*
+ * CompressorLZ4::Compress frame bytes (compressor.cc:15-65).
+ * frame = u32le(size_compressed_stored) u32le(size_source) payload.
+ * Writes the frame into `frame` (capacity >= 8 + max(bound, n)) and returns its
+ * length, or -1 where the reference returns IOError (ret <= 0).
+ */
+int64_t orc_frame_compress(const uint8_t* src, uint64_t n, uint8_t* frame) {
+  uint32_t bound = (uint32_t)orc_compress_bound((int)n);
+  int ret = orc_compress_limited(src, frame + 8, (int)n, (int)bound);
+  if (ret <= 0) return -1;                                      /* compressor.cc:31-34 */
+  uint32_t stored = (uint32_t)ret + 8;
+  uint64_t flen = (uint64_t)ret + 8;
+  if ((uint64_t)ret > n) {                                      /* compressor.cc:40-48 */
+    memcpy(frame + 8, src, n);
+    flen = n + 8;
+    stored = 0;
+  }
+  uint32_t n32 = (uint32_t)n;
+  for (int i = 0; i < 4; i++) { frame[i] = (uint8_t)(stored >> (8 * i)); frame[4 + i] = (uint8_t)(n32 >> (8 * i)); }
+  return (int64_t)flen;
+}
+
+/*
+ * CompressorLZ4::Uncompress of ONE frame at `frame` (compressor.cc:75-137),
+ * do_memory_allocation=false flavour.  Returns 0 (OK) and sets *out_n and
+ * *frame_n, or -1 (IOError) when the block decoder returns <= 0.
+ */
+int orc_frame_uncompress(const uint8_t* frame, uint8_t* out, uint64_t* out_n, uint64_t* frame_n) {
+  uint32_t stored = rd32(frame), raw = rd32(frame + 4);
+  if (stored > 0) {
+    uint32_t csz = stored - 8;
+    int ret = orc_decompress_safe_partial(frame + 8, out, (int)csz, (int)raw, (int)raw);
+    if (ret <= 0) return -1;
+    *out_n = (uint64_t)ret;
+    *frame_n = (uint64_t)csz + 8;
+  } else {
+    memcpy(out, frame + 8, raw);
+    *out_n = raw;
+    *frame_n = (uint64_t)raw + 8;
+  }
+  return 0;
+}
+
+/* ---- Generators ----------------------------------------------------------
+ * G1: db_bench's RandomGenerator (doc/bench/db_bench_kingdb.cc:113-142) over
+ * LevelDB's Random(301) (Park-Miller, A=16807, M=2^31-1) and
+ * test::CompressibleString(ratio 0.5, len 100) = 50 chars ' '+Uniform(95)
+ * repeated to 100.  LevelDB util/random.h + util/testutil.cc are not vendored in
+ * the reference; this restates their published algorithm (LevelDB 1.x).
+ */
+static inline uint32_t pm_next(uint32_t s) {
+  uint64_t product = (uint64_t)s * 16807u;
+  uint32_t r = (uint32_t)((product >> 31) + (product & 2147483647u));
+  if (r > 2147483647u) r -= 2147483647u;
+  return r;
+}
+/* Fills `out` with `npieces` 100-byte pieces starting from Random(seed). */
+void orc_g1_pieces(uint32_t seed, uint64_t npieces, uint8_t* out) {
+  uint32_t s = seed & 0x7fffffffu;
+  if (s == 0 || s == 2147483647u) s = 1;
+  for (uint64_t p = 0; p < npieces; p++) {
+    uint8_t raw[50];
+    for (int i = 0; i < 50; i++) { s = pm_next(s); raw[i] = (uint8_t)(' ' + s % 95); }
+    memcpy(out + p * 100, raw, 50);
+    memcpy(out + p * 100 + 50, raw, 50);
+  }
+}

@@ -1,0 +1,110 @@
+// oracle/ref_shim.cc -- TEST INFRASTRUCTURE ONLY (compiled into oracle/_ref/).
+//
+// A C-ABI wrapper, written for this repo, around the REFERENCE's own codec
+// objects (/root/reference/algorithm/{lz4,compressor,crc32c}.cc, compiled in
+// place by oracle/Makefile; no reference source is copied here).  It lets
+// tests/golden/make_golden.py drive the real reference through ctypes to emit
+// golden fixtures and to cross-check oracle/lz4_oracle.c.
+//
+// Also restates the two std::mt19937 generators of unit-tests/test_db.cc
+// (CompressibleDataGenerator 108-131 = G2, IncompressibleDataGenerator 87-105
+// = G3).  They depend only on libstdc++'s mt19937/uniform_int_distribution,
+// so running them here gives the same bytes the reference test harness sees.
+#include <cstdint>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "algorithm/compressor.h"
+#include "algorithm/crc32c.h"
+#include "algorithm/lz4.h"
+
+extern "C" {
+
+int ref_compress_bound(int n) { return LZ4_compressBound(n); }
+
+int ref_compress_limited(const char* src, char* dst, int n, int max_out) {
+  return LZ4_compress_limitedOutput(src, dst, n, max_out);
+}
+
+// Decodes a block placed in a zero-padded scratch buffer, so the (at most one)
+// byte the reference reads at iend is 0 -- the convention of the oracle and of
+// the GPU kernel.  The destination is zero-initialised for the same reason.
+int ref_decompress_partial(const char* src, int csize, char* dst, int target, int max_out) {
+  size_t n = csize > 0 ? (size_t)csize : 0;
+  std::vector<char> in(n + 64, 0);
+  if (n) memcpy(in.data(), src, n);
+  std::vector<char> out((size_t)(max_out > 0 ? max_out : 0) + 64, 0);
+  int ret = LZ4_decompress_safe_partial(in.data(), out.data(), csize, target, max_out);
+  if (ret > 0) memcpy(dst, out.data(), (size_t)ret);
+  return ret;
+}
+
+// CompressorLZ4::Compress: returns the frame length, or -1 on IOError.
+int64_t ref_frame_compress(const char* src, uint64_t n, char* frame_out) {
+  kdb::CompressorLZ4 c;
+  char* frame = nullptr;
+  uint64_t fn = 0;
+  kdb::Status s = c.Compress(const_cast<char*>(src), n, &frame, &fn);
+  if (!s.IsOK()) return -1;
+  memcpy(frame_out, frame, fn);
+  delete[] frame;
+  return (int64_t)fn;
+}
+
+// Streams CompressorLZ4::Uncompress over a concatenation of frames the way
+// unit-tests/test_compression.cc:100-115 does; returns the number of frames
+// decoded (or -1 on IOError) and writes the concatenated output.
+int64_t ref_frames_uncompress(const char* frames, uint64_t total, char* out, uint64_t* out_total) {
+  kdb::CompressorLZ4 c;
+  c.ResetThreadLocalStorage();
+  int64_t nframes = 0;
+  uint64_t pos = 0;
+  for (;;) {
+    char* dst = nullptr;
+    uint64_t dn = 0;
+    char* fr = nullptr;
+    uint64_t fn = 0;
+    kdb::Status s = c.Uncompress(const_cast<char*>(frames), total, &dst, &dn, &fr, &fn);
+    if (s.IsDone()) break;
+    if (!s.IsOK()) { delete[] dst; return -1; }
+    memcpy(out + pos, dst, dn);
+    pos += dn;
+    delete[] dst;
+    nframes++;
+  }
+  *out_total = pos;
+  return nframes;
+}
+
+uint32_t ref_crc32c_extend(uint32_t crc, const char* p, uint64_t n) {
+  return kdb::crc32c::Extend(crc, p, n);
+}
+
+// G2: test_db.cc:108-131, one generator instance, `count` successive calls.
+void ref_gen_g2(char* out, int size, int count) {
+  std::seed_seq seq{1, 2, 3, 4, 5, 6, 7};
+  std::mt19937 gen(seq);
+  std::uniform_int_distribution<int> dist(0, 255);
+  for (int v = 0; v < count; v++) {
+    char* data = out + (size_t)v * size;
+    int i = 0;
+    while (i < size) {
+      char ch = static_cast<char>(dist(gen));
+      int rep = dist(gen) % 30 + 1;
+      if (i + rep > size) rep = size - i;
+      memset(data + i, ch, rep);
+      i += rep;
+    }
+  }
+}
+
+// G3: test_db.cc:87-105.
+void ref_gen_g3(char* out, int size, int count) {
+  std::seed_seq seq{1, 2, 3, 4, 5, 6, 7};
+  std::mt19937 gen(seq);
+  std::uniform_int_distribution<int> dist(0, 255);
+  for (int64_t i = 0; i < (int64_t)size * count; i++) out[i] = static_cast<char>(dist(gen));
+}
+
+}  // extern "C"
