@@ -1,0 +1,132 @@
+/*
+ * include/kdb_lz4.h -- C ABI of the MI355X (gfx950) LZ4 block codec that drops in
+ * behind KingDB's CompressorLZ4 (/root/reference/algorithm/compressor.h:102-176).
+ *
+ * Plain pointers and sizes only; no HIP or torch types cross this boundary
+ * (streams and events are opaque `void*`).  Every function returns an int
+ * status (KDB_LZ4_OK or a negative KDB_LZ4_E* code) except where it mirrors an
+ * LZ4 r1.3.0 function, whose exact return convention it keeps.  No exception
+ * crosses the ABI.  The caller owns all memory.
+ *
+ * All compute runs in hand-written HIP kernels on the GPU.  There is no CPU
+ * codec behind this ABI: without a usable device the compute entry points
+ * return KDB_LZ4_ENODEV (scalar LZ4 mirrors: their error value) -- never a
+ * CPU result.
+ */
+#ifndef KDB_LZ4_H_
+#define KDB_LZ4_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KDB_LZ4_OK            0
+#define KDB_LZ4_EINVAL       -1   /* bad argument */
+#define KDB_LZ4_EHIP         -2   /* HIP runtime error (launch, copy, alloc) */
+#define KDB_LZ4_ENODEV       -3   /* no usable gfx950 device */
+#define KDB_LZ4_EUNSUPPORTED -4   /* size outside what this build's kernels handle */
+
+/* Per-value status word of the batch entry points for a value the launch
+ * could not process (e.g. larger than max_len); distinct from LZ4 codes. */
+#define KDB_LZ4_VALUE_UNSUPPORTED ((int32_t)0x80000000)
+
+int kdb_lz4_version(void); /* 10000*major + 100*minor + patch */
+
+/* ---------------------------------------------------------------- runtime */
+int kdb_lz4_device_count(int* count);
+int kdb_lz4_set_device(int device);
+int kdb_lz4_get_device(int* device);
+int kdb_lz4_malloc(void** ptr, uint64_t bytes);              /* device memory */
+int kdb_lz4_free(void* ptr);
+int kdb_lz4_host_alloc(void** ptr, uint64_t bytes);          /* pinned host memory */
+int kdb_lz4_host_free(void* ptr);
+int kdb_lz4_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream);
+int kdb_lz4_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream);
+int kdb_lz4_memcpy_d2d(void* dst, const void* src, uint64_t bytes, void* stream);
+int kdb_lz4_memset(void* ptr, int value, uint64_t bytes, void* stream);
+int kdb_lz4_stream_create(void** stream);
+int kdb_lz4_stream_destroy(void* stream);
+int kdb_lz4_stream_sync(void* stream);
+int kdb_lz4_device_sync(void);
+int kdb_lz4_event_create(void** event);
+int kdb_lz4_event_destroy(void* event);
+int kdb_lz4_event_record(void* event, void* stream);
+int kdb_lz4_event_sync(void* event);
+int kdb_lz4_event_elapsed_ms(void* start, void* stop, float* ms);
+
+/* ------------------------------------------------ scalar LZ4 r1.3.0 mirrors
+ * Host buffers, synchronous, one value per call (a batch of one on the GPU).
+ * Same signatures and return conventions as the reference; link-time aliases
+ * with the exact LZ4_* names are exported too. */
+
+/* replaces LZ4_compressBound, algorithm/lz4.h:115 (macro lz4.h:103) */
+int kdb_lz4_compressBound(int isize);
+
+/* replaces LZ4_compress_limitedOutput, algorithm/lz4.h:129 (lz4.cc:664-682):
+ * returns the block size, or 0 if it does not fit in maxOutputSize.  Unlike
+ * r1.3.0 this never writes past maxOutputSize. */
+int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize,
+                                   int maxOutputSize);
+
+/* replaces LZ4_decompress_safe_partial, algorithm/lz4.h:169 (lz4.cc:1050-1053):
+ * returns bytes decoded, or -(input bytes consumed)-1 on malformed input. */
+int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compressedSize,
+                                    int targetOutputSize, int maxDecompressedSize);
+
+/* ------------------------------------------------------- batch entry points
+ * Device pointers; stream-ordered and asynchronous (`stream` may be NULL for
+ * the default stream).  Value v occupies src[src_off[v] .. +len[v]) and writes
+ * dst[dst_off[v] ..).  `max_len` (compress) / `max_in`,`max_out` (decompress)
+ * bound the per-value sizes of the launch; they size the kernels' LDS. */
+
+/* 8 + LZ4_compressBound(size): the slot a CompressorLZ4 frame needs. */
+uint64_t kdb_lz4_frame_bound(uint32_t size);
+
+/* LZ4_compress_limitedOutput per value: ret[v] = block size or 0;
+ * dst slot capacity dst_cap[v]. */
+int kdb_lz4_compress_blocks_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint32_t n, uint32_t max_len,
+                                  uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_cap,
+                                  int32_t* ret);
+
+/* LZ4_decompress_safe_partial(src, dst, in_len, target, dst_cap) per value
+ * (target == NULL means target = dst_cap); ret[v] = LZ4 return code. */
+int kdb_lz4_decompress_blocks_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                    const uint32_t* in_len, uint32_t n, uint32_t max_in,
+                                    uint32_t max_out, uint8_t* dst, const uint64_t* dst_off,
+                                    const uint32_t* dst_cap, const uint32_t* target,
+                                    int32_t* ret);
+
+/* CompressorLZ4::Compress per value (compressor.cc:15-65): frame = u32le
+ * size_compressed_stored, u32le size_source, payload (raw fallback when the
+ * block is larger than the value).  Slot capacity >= kdb_lz4_frame_bound(len).
+ * frame_len[v] = frame bytes; status[v] = 0, or -1 where the reference returns
+ * IOError. */
+int kdb_lz4_compress_frames_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint32_t n, uint32_t max_len,
+                                  uint8_t* dst, const uint64_t* dst_off, uint32_t* frame_len,
+                                  int32_t* status);
+
+/* CompressorLZ4::Uncompress of one frame per value (compressor.cc:75-137):
+ * avail[v] = bytes readable at src_off[v]; raw bytes go to dst_off[v] (capacity
+ * dst_cap[v]); out_len[v] = *size_dest; status[v] = 0 or -1 (IOError). */
+int kdb_lz4_decompress_frames_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                    const uint32_t* avail, uint32_t n, uint32_t max_in,
+                                    uint32_t max_out, uint8_t* dst, const uint64_t* dst_off,
+                                    const uint32_t* dst_cap, uint32_t* out_len, int32_t* status);
+
+/* ----------------------------------------------------------- data helpers */
+
+/* Synthetic G1 ("db_bench") data on the device: 100-byte pieces first_piece ..
+ * first_piece+npieces-1 of LevelDB Random(seed) CompressibleString(0.5, 100)
+ * (doc/bench/db_bench_kingdb.cc:119-131), generated in parallel by jump-ahead. */
+int kdb_lz4_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KDB_LZ4_H_ */

@@ -1,0 +1,113 @@
+// kingdb_amd/csrc/compressor.h -- drop-in replacement for KingDB's CompressorLZ4
+// (/root/reference/algorithm/compressor.h:102-176).
+//
+// Same class name, namespace, public methods, frame format, Status codes and
+// buffer-ownership rules as the reference; the LZ4 work runs in the gfx950
+// kernels through include/kdb_lz4.h.  Per-thread stream state (the reference's
+// ThreadStorage, thread/threadstorage.h:23-46) is kept per (instance, thread).
+//
+// Added (not replacing): CompressFrames / UncompressFrames, which move a whole
+// batch of values through one H2D copy, one kernel launch and one D2H copy.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "kdb_types.h"
+
+namespace kdb {
+
+// thread/threadstorage.h:23-46: one uint64_t per calling thread, default 0.
+class ThreadStorageLZ4 {
+ public:
+  uint64_t get() {
+    std::lock_guard<std::mutex> l(mu_);
+    return v_[std::this_thread::get_id()];
+  }
+  void put(uint64_t x) {
+    std::lock_guard<std::mutex> l(mu_);
+    v_[std::this_thread::get_id()] = x;
+  }
+  void reset() { put(0); }
+
+ private:
+  std::mutex mu_;
+  std::map<std::thread::id, uint64_t> v_;
+};
+
+// algorithm/crc32c.h:74-103: CRC32C stream state per thread.
+class CRC32LZ4 {
+ public:
+  void stream(const char* data, size_t n);
+  uint32_t get() { return (uint32_t)ts_.get(); }
+  void put(uint32_t c) { ts_.put(c); }
+  void ResetThreadLocalStorage() { ts_.reset(); }
+
+ private:
+  ThreadStorageLZ4 ts_;
+};
+
+uint32_t Crc32cExtend(uint32_t crc, const char* data, size_t n);
+
+class CompressorLZ4 {
+ public:
+  CompressorLZ4() {}
+  // compressor.h:110-113: assignment does not copy state.
+  CompressorLZ4& operator=(const CompressorLZ4&) { return *this; }
+  virtual ~CompressorLZ4() {}
+
+  void ResetThreadLocalStorage();
+
+  Status Compress(char* raw_in, uint64_t size_raw_in, char** compressed_out, uint64_t* size_compressed_out);
+
+  bool IsUncompressionDone(uint64_t size_source);
+  Status Uncompress(char* source, uint64_t size_source, char** dest, uint64_t* size_dest, char** frame_out,
+                    uint64_t* size_frame_out, bool do_memory_allocation = true);
+
+  Status UncompressByteArray(ByteArray& value, bool do_checksum_verification, ByteArray* value_uncompressed);
+
+  void DisableCompressionInFrameHeader(char* frame) {
+    for (uint64_t i = 0; i < size_frame_header(); i++) frame[i] = 0;
+  }
+  bool HasFrameHeaderDisabledCompression(char* frame) {
+    for (uint64_t i = 0; i < size_frame_header(); i++)
+      if (frame[i] != 0) return false;
+    return true;
+  }
+  uint64_t size_compressed() { return ts_compress_.get(); }
+  uint64_t MaxInputSize() { return 0x7E000000; }  // LZ4_MAX_INPUT_SIZE, lz4.h:102
+  uint64_t size_frame_header() { return 8; }
+  uint64_t size_uncompressed_frame(uint64_t size_data) { return size_data + 8; }
+  void AdjustCompressedSize(int64_t inc) {
+    int64_t size = ts_compress_.get() + inc;
+    ts_compress_.put(size);
+  }
+
+  // ---- batch additions -------------------------------------------------
+  // Compresses n independent values (one frame each) in one GPU launch.
+  // frames[i] receives a new[] buffer (caller delete[]s), like Compress().
+  // Does not touch the per-thread stream offsets.
+  Status CompressFrames(uint32_t n, char* const* raw_in, const uint64_t* size_raw_in, char** frames,
+                        uint64_t* frame_sizes);
+  // Decodes n single frames in one launch into caller buffers out[i] of
+  // out_cap[i] bytes; size_out[i] = *size_dest.  Per-frame failures are
+  // reported in the returned Status (first failing index in message).
+  Status UncompressFrames(uint32_t n, char* const* frames, const uint64_t* frame_avail, char* const* out,
+                          const uint64_t* out_cap, uint64_t* size_out);
+
+  // Reference quirk: Uncompress() always streams each frame
+  // into crc32_ and UncompressByteArray() streams it again when verifying, so
+  // verification of a compressed value fails.  true (default) = bug-for-bug.
+  void set_crc_double_stream(bool on) { crc_double_stream_ = on; }
+
+ private:
+  ThreadStorageLZ4 ts_compress_;
+  ThreadStorageLZ4 ts_uncompress_;
+  CRC32LZ4 crc32_;
+  bool crc_double_stream_ = true;
+};
+
+}  // namespace kdb

@@ -1,0 +1,291 @@
+// kingdb_amd/csrc/kdb_lz4_capi.hip -- the C ABI declared in include/kdb_lz4.h.
+//
+// Batch entry points launch the gfx950 kernels on the caller's stream.  The
+// scalar LZ4 mirrors (one value per call, host buffers) go through the same
+// kernels as a batch of one, using a per-thread, per-device staging context
+// (pinned host + device buffers + a private stream) that grows on demand.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+
+#include "../../include/kdb_lz4.h"
+#include "lz4_device.h"
+
+namespace kdb_lz4 {
+hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
+                           const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
+                           const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
+                           int32_t* ret);
+hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
+                             const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
+                             uint8_t* dst, const uint64_t* dst_off, const uint32_t* out_cap,
+                             const uint32_t* target, uint32_t* out_len, int32_t* ret);
+hipError_t launch_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed,
+                         hipStream_t st);
+}  // namespace kdb_lz4
+
+using namespace kdb_lz4;
+
+namespace {
+
+inline int hip_status(hipError_t e) {
+  if (e == hipSuccess) return KDB_LZ4_OK;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorInsufficientDriver)
+    return KDB_LZ4_ENODEV;
+  return KDB_LZ4_EHIP;
+}
+
+// Largest value the byU16 kernels take (lz4.cc:673: S < 65547).
+constexpr uint32_t kMaxKernelValue = k64KLimit - 1u;
+
+// Per-thread, per-device context of the scalar entry points.
+struct ScalarCtx {
+  hipStream_t stream = nullptr;
+  uint8_t* dev = nullptr;     // [meta 64 B][in][out]
+  uint8_t* host = nullptr;    // pinned mirror
+  size_t cap = 0;
+  ~ScalarCtx() {
+    if (dev) (void)hipFree(dev);
+    if (host) (void)hipHostFree(host);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+  int reserve(size_t bytes) {
+    if (!stream) {
+      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return KDB_LZ4_EHIP;
+    }
+    if (bytes <= cap) return KDB_LZ4_OK;
+    size_t want = cap ? cap : 1u << 16;
+    while (want < bytes) want *= 2;
+    if (dev) (void)hipFree(dev);
+    if (host) (void)hipHostFree(host);
+    dev = nullptr;
+    host = nullptr;
+    cap = 0;
+    if (hipMalloc(&dev, want) != hipSuccess) return KDB_LZ4_EHIP;
+    if (hipHostMalloc(&host, want, hipHostMallocDefault) != hipSuccess) return KDB_LZ4_EHIP;
+    cap = want;
+    return KDB_LZ4_OK;
+  }
+};
+
+ScalarCtx& scalar_ctx(int* err) {
+  thread_local std::unordered_map<int, ScalarCtx> ctxs;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  *err = hip_status(e);
+  return ctxs[dev];
+}
+
+// Layout of the scalar staging buffer: a 64-byte metadata block (offsets,
+// lengths, caps, results) followed by input and output regions.
+struct Meta {
+  uint64_t src_off, dst_off;
+  uint32_t len, cap, target, out_len;
+  int32_t ret, pad;
+};
+static_assert(sizeof(Meta) <= 64, "meta block");
+constexpr size_t kMetaBytes = 64;
+
+inline size_t align16(size_t x) { return (x + 15u) & ~(size_t)15u; }
+
+}  // namespace
+
+extern "C" {
+
+int kdb_lz4_version(void) { return 10000; }
+
+int kdb_lz4_device_count(int* count) {
+  if (!count) return KDB_LZ4_EINVAL;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *count = e == hipSuccess ? n : 0;
+  return e == hipSuccess ? KDB_LZ4_OK : KDB_LZ4_ENODEV;
+}
+int kdb_lz4_set_device(int device) { return hip_status(hipSetDevice(device)); }
+int kdb_lz4_get_device(int* device) { return device ? hip_status(hipGetDevice(device)) : KDB_LZ4_EINVAL; }
+int kdb_lz4_malloc(void** ptr, uint64_t bytes) {
+  return ptr ? hip_status(hipMalloc(ptr, bytes ? bytes : 1)) : KDB_LZ4_EINVAL;
+}
+int kdb_lz4_free(void* ptr) { return hip_status(hipFree(ptr)); }
+int kdb_lz4_host_alloc(void** ptr, uint64_t bytes) {
+  return ptr ? hip_status(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault)) : KDB_LZ4_EINVAL;
+}
+int kdb_lz4_host_free(void* ptr) { return hip_status(hipHostFree(ptr)); }
+int kdb_lz4_memcpy_h2d(void* dst, const void* src, uint64_t bytes, void* stream) {
+  return hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+}
+int kdb_lz4_memcpy_d2h(void* dst, const void* src, uint64_t bytes, void* stream) {
+  return hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+}
+int kdb_lz4_memcpy_d2d(void* dst, const void* src, uint64_t bytes, void* stream) {
+  return hip_status(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}
+int kdb_lz4_memset(void* ptr, int value, uint64_t bytes, void* stream) {
+  return hip_status(hipMemsetAsync(ptr, value, bytes, (hipStream_t)stream));
+}
+int kdb_lz4_stream_create(void** stream) {
+  return stream ? hip_status(hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking))
+                : KDB_LZ4_EINVAL;
+}
+int kdb_lz4_stream_destroy(void* stream) { return hip_status(hipStreamDestroy((hipStream_t)stream)); }
+int kdb_lz4_stream_sync(void* stream) { return hip_status(hipStreamSynchronize((hipStream_t)stream)); }
+int kdb_lz4_device_sync(void) { return hip_status(hipDeviceSynchronize()); }
+int kdb_lz4_event_create(void** event) {
+  return event ? hip_status(hipEventCreate((hipEvent_t*)event)) : KDB_LZ4_EINVAL;
+}
+int kdb_lz4_event_destroy(void* event) { return hip_status(hipEventDestroy((hipEvent_t)event)); }
+int kdb_lz4_event_record(void* event, void* stream) {
+  return hip_status(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+}
+int kdb_lz4_event_sync(void* event) { return hip_status(hipEventSynchronize((hipEvent_t)event)); }
+int kdb_lz4_event_elapsed_ms(void* start, void* stop, float* ms) {
+  return ms ? hip_status(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop)) : KDB_LZ4_EINVAL;
+}
+
+// ------------------------------------------------------------------ scalar
+int kdb_lz4_compressBound(int isize) { return (int)compress_bound((uint32_t)isize); }
+
+int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize, int maxOutputSize) {
+  if ((uint32_t)inputSize > kMaxInput) return 0;                 // lz4.cc:465
+  if (maxOutputSize < 0) maxOutputSize = 0;
+  if ((uint32_t)inputSize > kMaxKernelValue) return 0;           // byU32 sizes: not in this build
+  int err = 0;
+  ScalarCtx& c = scalar_ctx(&err);
+  if (err) return 0;
+  const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)inputSize + 16);
+  // The kernel never writes past the cap, and the cap never needs to exceed
+  // the bound for the return value to be exact.
+  const uint32_t bound = compress_bound((uint32_t)inputSize);
+  const uint32_t cap = (uint32_t)maxOutputSize < bound ? (uint32_t)maxOutputSize : bound;
+  if (c.reserve(out_at + align16(cap + 16)) != KDB_LZ4_OK) return 0;
+  Meta m{};
+  m.src_off = in_at;
+  m.dst_off = out_at;
+  m.len = (uint32_t)inputSize;
+  m.cap = (uint32_t)maxOutputSize;
+  memcpy(c.host, &m, sizeof(m));
+  if (inputSize) memcpy(c.host + in_at, source, (size_t)inputSize);
+  Meta* dm = reinterpret_cast<Meta*>(c.dev);
+  if (hipMemcpyAsync(c.dev, c.host, in_at + (size_t)inputSize, hipMemcpyHostToDevice, c.stream) != hipSuccess)
+    return 0;
+  if (launch_compress(false, c.stream, c.dev, &dm->src_off, &dm->len, 1, (uint32_t)inputSize, c.dev,
+                      &dm->dst_off, &dm->cap, nullptr, &dm->ret) != hipSuccess)
+    return 0;
+  if (hipMemcpyAsync(c.host, c.dev, kMetaBytes, hipMemcpyDeviceToHost, c.stream) != hipSuccess) return 0;
+  if (hipStreamSynchronize(c.stream) != hipSuccess) return 0;
+  memcpy(&m, c.host, sizeof(m));
+  if (m.ret > 0) {
+    if (hipMemcpyAsync(c.host + out_at, c.dev + out_at, (size_t)m.ret, hipMemcpyDeviceToHost, c.stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(c.stream) != hipSuccess)
+      return 0;
+    memcpy(dest, c.host + out_at, (size_t)m.ret);
+  }
+  return m.ret > 0 ? m.ret : 0;
+}
+
+int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compressedSize,
+                                    int targetOutputSize, int maxDecompressedSize) {
+  // Sizes the kernel cannot take are reported like a malformed block at byte 0.
+  if (compressedSize < 0 || maxDecompressedSize < 0 || (uint32_t)maxDecompressedSize > kMaxKernelValue)
+    return -1;
+  int err = 0;
+  ScalarCtx& c = scalar_ctx(&err);
+  if (err) return -1;
+  const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)compressedSize + 16);
+  if (c.reserve(out_at + align16((size_t)maxDecompressedSize + 16)) != KDB_LZ4_OK) return -1;
+  Meta m{};
+  m.src_off = in_at;
+  m.dst_off = out_at;
+  m.len = (uint32_t)compressedSize;
+  m.cap = (uint32_t)maxDecompressedSize;
+  m.target = (uint32_t)targetOutputSize;
+  memcpy(c.host, &m, sizeof(m));
+  if (compressedSize) memcpy(c.host + in_at, source, (size_t)compressedSize);
+  Meta* dm = reinterpret_cast<Meta*>(c.dev);
+  if (hipMemcpyAsync(c.dev, c.host, in_at + (size_t)compressedSize, hipMemcpyHostToDevice, c.stream) !=
+      hipSuccess)
+    return -1;
+  if (launch_decompress(false, c.stream, c.dev, &dm->src_off, &dm->len, 1, (uint32_t)compressedSize,
+                        (uint32_t)maxDecompressedSize, c.dev, &dm->dst_off, &dm->cap, &dm->target,
+                        &dm->out_len, &dm->ret) != hipSuccess)
+    return -1;
+  if (hipMemcpyAsync(c.host, c.dev, kMetaBytes, hipMemcpyDeviceToHost, c.stream) != hipSuccess) return -1;
+  if (hipStreamSynchronize(c.stream) != hipSuccess) return -1;
+  memcpy(&m, c.host, sizeof(m));
+  if (m.ret == KDB_LZ4_VALUE_UNSUPPORTED) return -1;
+  if (m.ret > 0) {
+    if (hipMemcpyAsync(c.host + out_at, c.dev + out_at, (size_t)m.ret, hipMemcpyDeviceToHost, c.stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(c.stream) != hipSuccess)
+      return -1;
+    memcpy(dest, c.host + out_at, (size_t)m.ret);
+  }
+  return m.ret;
+}
+
+// ------------------------------------------------------------------- batch
+uint64_t kdb_lz4_frame_bound(uint32_t size) { return 8u + (uint64_t)compress_bound(size); }
+
+int kdb_lz4_compress_blocks_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
+                                  const uint64_t* dst_off, const uint32_t* dst_cap, int32_t* ret) {
+  if (n == 0) return KDB_LZ4_OK;
+  if (!src || !src_off || !src_len || !dst || !dst_off || !dst_cap || !ret) return KDB_LZ4_EINVAL;
+  if (max_len > kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
+  return hip_status(launch_compress(false, (hipStream_t)stream, src, src_off, src_len, n, max_len, dst,
+                                    dst_off, dst_cap, nullptr, ret));
+}
+
+int kdb_lz4_decompress_blocks_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                    const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
+                                    uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_cap,
+                                    const uint32_t* target, int32_t* ret) {
+  if (n == 0) return KDB_LZ4_OK;
+  if (!src || !src_off || !in_len || !dst || !dst_off || !dst_cap || !ret) return KDB_LZ4_EINVAL;
+  if (max_out > kMaxKernelValue || max_in > 2u * kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
+  return hip_status(launch_decompress(false, (hipStream_t)stream, src, src_off, in_len, n, max_in, max_out,
+                                      dst, dst_off, dst_cap, target, nullptr, ret));
+}
+
+int kdb_lz4_compress_frames_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                  const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
+                                  const uint64_t* dst_off, uint32_t* frame_len, int32_t* status) {
+  if (n == 0) return KDB_LZ4_OK;
+  if (!src || !src_off || !src_len || !dst || !dst_off || !frame_len || !status) return KDB_LZ4_EINVAL;
+  if (max_len > kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
+  return hip_status(launch_compress(true, (hipStream_t)stream, src, src_off, src_len, n, max_len, dst,
+                                    dst_off, nullptr, frame_len, status));
+}
+
+int kdb_lz4_decompress_frames_batch(void* stream, const uint8_t* src, const uint64_t* src_off,
+                                    const uint32_t* avail, uint32_t n, uint32_t max_in, uint32_t max_out,
+                                    uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_cap,
+                                    uint32_t* out_len, int32_t* status) {
+  if (n == 0) return KDB_LZ4_OK;
+  if (!src || !src_off || !avail || !dst || !dst_off || !dst_cap || !out_len || !status)
+    return KDB_LZ4_EINVAL;
+  if (max_out > kMaxKernelValue || max_in > 2u * kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
+  return hip_status(launch_decompress(true, (hipStream_t)stream, src, src_off, avail, n, max_in, max_out,
+                                      dst, dst_off, dst_cap, nullptr, out_len, status));
+}
+
+int kdb_lz4_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed, void* stream) {
+  if (!dst) return KDB_LZ4_EINVAL;
+  return hip_status(launch_gen_g1(dst, first_piece, npieces, seed, (hipStream_t)stream));
+}
+
+// Link-time aliases with the reference's exact C names (algorithm/lz4.h:36-38,
+// extern "C"), so an object built against lz4.h links against this library.
+int LZ4_compressBound(int isize) { return kdb_lz4_compressBound(isize); }
+int LZ4_compress_limitedOutput(const char* s, char* d, int n, int m) {
+  return kdb_lz4_compress_limitedOutput(s, d, n, m);
+}
+int LZ4_decompress_safe_partial(const char* s, char* d, int c, int t, int m) {
+  return kdb_lz4_decompress_safe_partial(s, d, c, t, m);
+}
+
+}  // extern "C"

@@ -1,0 +1,101 @@
+// kingdb_amd/csrc/lz4_device.h -- device-side building blocks shared by the
+// gfx950 LZ4 compress / decompress kernels.
+//
+// Execution model (CDNA4, wave64): one wavefront owns one value.  Control flow
+// of the LZ4 parse is wave-uniform (every scalar below is the same in all 64
+// lanes and is pinned to SGPRs with readfirstlane); the lanes cooperate on the
+// byte work -- staging, literal/match copies, match-length scans (ballot +
+// ctz), catch-up scans and the speculative 64-position hash search.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kdb_lz4 {
+
+// LZ4 r1.3.0 constants (/root/reference/algorithm/lz4.cc:222-246, lz4.h:102).
+constexpr uint32_t kMinMatch = 4;
+constexpr uint32_t kLastLiterals = 5;
+constexpr uint32_t kMfLimit = 12;
+constexpr uint32_t kMinLength = 13;
+constexpr uint32_t k64KLimit = 65536u + 11u;   // byU16 iff S < this (lz4.cc:673)
+constexpr uint32_t kMaxDistance = 65535u;
+constexpr uint32_t kRunMask = 15u;
+constexpr uint32_t kMlMask = 15u;
+constexpr uint32_t kMaxInput = 0x7E000000u;
+constexpr uint32_t kHash16Entries = 8192u;    // 13-bit byU16 hash (lz4.cc:376)
+constexpr uint32_t kTableBytes = kHash16Entries * 2u;
+
+// Status word for values a launch cannot process (distinct from every LZ4
+// return code, which is >= -(csize+1)).
+constexpr int32_t kUnsupported = INT32_MIN;
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+}
+__device__ __forceinline__ int unii(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ uint32_t readlane(uint32_t x, uint32_t l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
+}
+
+// Lanes-below / lanes-up-to masks (lane in 0..63; 2ull<<63 wraps to 0 -> ~0).
+__device__ __forceinline__ uint64_t mask_lt(uint32_t l) { return (1ull << l) - 1ull; }
+__device__ __forceinline__ uint64_t mask_le(uint32_t l) { return (2ull << l) - 1ull; }
+
+// Index of the first zero lane in a ballot, 64 if none.
+__device__ __forceinline__ uint32_t first_zero(uint64_t m) {
+  uint64_t z = ~m;
+  return z ? (uint32_t)__builtin_ctzll(z) : 64u;
+}
+
+// LZ4_compressBound (lz4.h:103).
+__host__ __device__ __forceinline__ uint32_t compress_bound(uint32_t n) {
+  return n > kMaxInput ? 0u : n + n / 255u + 16u;
+}
+
+// Unaligned little-endian u32 at byte offset b of a 16B-aligned LDS buffer
+// that is readable for 4 bytes past b+3 (two aligned dwords + v_alignbyte).
+__device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t b) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds);
+  uint32_t q = b >> 2;
+  return __builtin_amdgcn_alignbyte(w[q + 1], w[q], b & 3u);
+}
+
+// Copies n bytes at global g (any alignment) into the 16B-aligned LDS buffer
+// `lds` with whole aligned 16-byte loads; byte i of the value lands at
+// lds[head + i] with head = g & 15 (returned).  An aligned 16-byte chunk never
+// crosses a page, so the over-read around [g, g+n) cannot fault.
+__device__ __forceinline__ uint32_t stage_to_lds(const uint8_t* g, uint32_t n, uint8_t* lds) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(g);
+  const uint32_t head = (uint32_t)(a & 15u);
+  const uint4* base = reinterpret_cast<const uint4*>(a - head);
+  const uint32_t chunks = (head + n + 15u) >> 4;
+  uint4* l = reinterpret_cast<uint4*>(lds);
+  for (uint32_t c = lane_id(); c < chunks; c += 64u) l[c] = base[c];
+  return head;
+}
+
+// Stores n bytes from LDS (value byte i at lds[head + i]) to global g (any
+// alignment): byte stores for the unaligned head/tail, dword stores between.
+__device__ __forceinline__ void flush_from_lds(uint8_t* g, const uint8_t* lds, uint32_t head,
+                                               uint32_t n) {
+  const uint32_t lane = lane_id();
+  const uint32_t mis = (uint32_t)((4u - (reinterpret_cast<uintptr_t>(g) & 3u)) & 3u);
+  const uint32_t pre = mis < n ? mis : n;
+  if (lane < pre) g[lane] = lds[head + lane];
+  const uint32_t body = (n - pre) >> 2;
+  uint32_t* gw = reinterpret_cast<uint32_t*>(g + pre);
+  const uint32_t sb = head + pre;
+  if ((sb & 3u) == 0) {
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds + sb);
+    for (uint32_t i = lane; i < body; i += 64u) gw[i] = lw[i];
+  } else {
+    for (uint32_t i = lane; i < body; i += 64u) gw[i] = lds_rd32(lds, sb + 4u * i);
+  }
+  const uint32_t done = pre + 4u * body;
+  if (lane < n - done) g[done + lane] = lds[head + done + lane];
+}
+
+}  // namespace kdb_lz4

@@ -1,0 +1,159 @@
+"""GPU: the gfx950 kernels (through the C ABI) against the reference-generated
+golden fixtures and the oracle.  Bit-exact for every byte and return code."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_golden, split
+
+pytestmark = pytest.mark.gpu
+
+
+def test_kat_blocks_frames(gpu):
+    g = load_golden("kat_blocks.npz")
+    inputs = split(g["inp"], g["inp_off"], g["inp_len"])
+    blocks = split(g["blk"], g["blk_off"], g["blk_len"])
+    frames = split(g["frm"], g["frm_off"], g["frm_len"])
+    got = gpu.compress_blocks(inputs)
+    for name, (r, b), exp in zip(g["names"], got, blocks):
+        assert r == len(exp) and b == exp, name
+    assert gpu.compress_frames(inputs) == frames
+    dec = gpu.decompress_blocks(blocks, [len(x) for x in inputs])
+    for name, (r, out), x in zip(g["names"], dec, inputs):
+        assert r == len(x) and out == x, name
+    fdec = gpu.decompress_frames(frames, [len(x) for x in inputs])
+    for name, (st, out), x in zip(g["names"], fdec, inputs):
+        assert st == 0 and out == x, name
+
+
+def test_limited_output(gpu):
+    g = load_golden("limited_output.npz")
+    inputs = split(g["inp"], g["inp_off"], g["inp_len"])
+    got = gpu.compress_blocks(inputs, caps=[int(c) for c in g["cap"]])
+    for i, ((r, b), ret) in enumerate(zip(got, g["ret"])):
+        assert r == int(ret), i
+        if r:
+            o = int(g["blk_off"][i])
+            assert b == g["blk"][o:o + r].tobytes(), i
+
+
+def test_malformed_return_codes(gpu):
+    g = load_golden("malformed.npz")
+    blocks = split(g["blk"], g["blk_off"], g["blk_len"])
+    sizes = [int(s) for s in g["size"]]
+    targets = [int(t) for t in g["target"]]
+    got = gpu.decompress_blocks(blocks, sizes, targets)
+    for i, (r, out) in enumerate(got):
+        assert r == int(g["ret"][i]), (i, r, int(g["ret"][i]))
+        if r > 0 and g["cmp"][i]:
+            o = int(g["out_off"][i])
+            assert out == g["out"][o:o + r].tobytes(), i
+
+
+def test_g1_db_bench_values(gpu, orc):
+    """db_bench G1 values (SURVEY KATs T3-T5) compressed in one launch per size."""
+    g = load_golden("g1_db_bench.npz")
+    pool = oracle.g1_pool(orc)
+    for size, count in ((100, 1000), (4096, 1000), (65536, 16)):
+        vals = oracle.g1_values(pool, size, count)
+        got = gpu.compress_blocks(vals)
+        assert [r for r, _ in got] == list(g[f"s{size}_blk_len"])
+        assert orc.crc32c(b"".join(b for _, b in got)) == int(g[f"s{size}_blk_crc"][0])
+        frames = gpu.compress_frames(vals)
+        assert [len(f) for f in frames] == list(g[f"s{size}_frm_len"])
+        assert orc.crc32c(b"".join(frames)) == int(g[f"s{size}_frm_crc"][0])
+        back = gpu.decompress_frames(frames, [size] * count)
+        assert all(st == 0 and out == v for (st, out), v in zip(back, vals))
+
+
+def test_test_db_generators(gpu):
+    g = load_golden("test_db_generators.npz")
+    for name in ("g2", "g3"):
+        for size in (100, 4096):
+            data = g[f"{name}_{size}_inp"]
+            lens = g[f"{name}_{size}_frm_len"]
+            off = np.concatenate([[0], np.cumsum(lens)[:-1]])
+            frames = split(g[f"{name}_{size}_frm"], off, lens)
+            vals = [data[i * size:(i + 1) * size].tobytes() for i in range(len(lens))]
+            assert gpu.compress_frames(vals) == frames
+            back = gpu.decompress_frames(frames, [size] * len(vals))
+            assert all(st == 0 and out == v for (st, out), v in zip(back, vals))
+
+
+def test_test_compression_shape(gpu):
+    """unit-tests/test_compression.cc:43-125 on the GPU path."""
+    g = load_golden("test_compression.npz")
+    key = b"0x10c095000-0"
+    value = (key * (442837 // len(key) + 1))[:442837]
+    chunks = [value[i:i + 65536] for i in range(0, len(value), 65536)]
+    frames = gpu.compress_frames(chunks)
+    assert b"".join(frames) == g["frames"].tobytes()
+    back = gpu.decompress_frames(frames, [len(c) for c in chunks])
+    assert b"".join(out for _, out in back) == value
+
+
+def test_scalar_mirrors(gpu, orc):
+    rng = random.Random(5)
+    for n in (0, 1, 12, 13, 100, 4096, 65546):
+        x = bytes(rng.choice(b"abcd") for _ in range(n))
+        bound = orc.compress_bound(n)
+        r, b = gpu.compress_limited_output(x, bound)
+        assert b == orc.compress(x)
+        assert gpu.decompress_safe_partial(b, n, n) == (n, x) if n else True
+        r2, _ = gpu.compress_limited_output(x, max(bound // 3, 0))
+        exp = orc.compress(x, max(bound // 3, 0))
+        assert r2 == (0 if exp is None else len(exp))
+
+
+def test_random_vs_oracle(gpu, orc):
+    rng = random.Random(2024)
+    vals = []
+    for _ in range(400):
+        n = rng.choice([rng.randrange(0, 64), rng.randrange(64, 5000), rng.randrange(5000, 65547)])
+        k = rng.randrange(4)
+        if k == 0:
+            v = bytes(rng.randrange(256) for _ in range(min(n, 3000))) * (n // 3000 + 1)
+        elif k == 1:
+            v = bytes(rng.choice(b"xy") for _ in range(n))
+        elif k == 2:
+            p = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 70)))
+            v = p * (n // len(p) + 1)
+        else:
+            v = bytes(min(255, int(rng.expovariate(0.2))) for _ in range(n))
+        vals.append(v[:n])
+    got = gpu.compress_frames(vals)
+    for v, f in zip(vals, got):
+        assert f == orc.frame(v)
+
+
+def test_device_g1_generator_matches_oracle(gpu, orc):
+    from kingdb_amd.lz4 import DeviceBuffer, lib
+    d = DeviceBuffer(1000 * 100)
+    assert lib().kdb_lz4_gen_g1(d.ptr, 0, 1000, 301, None) == 0
+    assert d.download(100000).tobytes() == orc.g1_pieces(1000).tobytes()
+    assert lib().kdb_lz4_gen_g1(d.ptr, 123456, 10, 301, None) == 0
+    assert d.download(1000).tobytes() == orc.g1_pieces(123466)[123456 * 100:].tobytes()
+
+
+def test_device_batch_roundtrip_g1_long(gpu, orc):
+    """64Ki x 4 KiB G1-long values resident in HBM: frames byte-identical to the
+    oracle on a sample, full round trip bit-exact (size-independent property)."""
+    n, size = 65536, 4096
+    b = gpu.DeviceBatch.g1_long(n, size)
+    b.compress()
+    b.decompress()
+    cst, dst = b.status()
+    assert (cst == 0).all() and (dst == 0).all()
+    assert (b.out_lens() == size).all()
+    src = b.src.download(n * size)
+    out = b.out.download(n * size)
+    assert np.array_equal(src, out)
+    flen = b.frame_lens()
+    frames = b.frames.download(n * b.slot)
+    for i in list(range(0, n, 997)) + [n - 1]:
+        exp = orc.frame(src[i * size:(i + 1) * size].tobytes())
+        got = frames[i * b.slot:i * b.slot + int(flen[i])].tobytes()
+        assert got == exp, i
+    b.free()
