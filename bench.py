@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py -- LZ4 compress+decompress GiB/s (device-resident), batched 4 KiB values.
+
+BASELINE.json metric on its single-GPU config: 1M x 4 KiB values ("configs"[2]:
+round trip, frames byte-identical to the reference).  One *step* = one
+CompressorLZ4 frame-compress launch over the whole batch followed by one
+frame-decompress launch of the frames it produced (the kernels in
+kingdb_amd/csrc); inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+For N > 1 the driver starts one process per GPU with torch.distributed.run;
+each rank owns its own shard of G1-long values (no collective on the data
+path -- LZ4 blocks are independent); gloo carries only the
+barrier and the max-over-ranks of the elapsed time.  `value` is the raw bytes
+all ranks processed / max elapsed.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "LZ4 compress+decompress GiB/s (device-resident), batched 4 KiB values, 1/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--values", type=int, default=1 << 20, help="values per GPU")
+    p.add_argument("--size", type=int, default=4096, help="bytes per value")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU leg")
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="HBM traffic summary written by tools/pmc_traffic.py")
+    return p.parse_args()
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(sample: np.ndarray, size: int, seconds: float) -> dict:
+    """Times the reference's algorithm/lz4.cc (oracle/_ref, kind "reference")
+    or, where that build is absent, the oracle restatement (kind "port") on the
+    host cores, on a bounded sample of the same G1-long values."""
+    import oracle  # checker / baseline only
+    ref_so = oracle.REF_SO
+    if os.path.exists(ref_so):
+        lib = ctypes.CDLL(ref_so)
+        fn, kind = lib.ref_bench_roundtrip, "reference"
+    else:
+        lib = ctypes.CDLL(oracle.Oracle().lib._name)
+        fn, kind = lib.orc_bench_roundtrip, "port"
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                   ctypes.POINTER(ctypes.c_uint64)]
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+
+    def run(n, th, passes):
+        tc, td, cb = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        rc = fn(sample.ctypes.data, n, size, th, passes, ctypes.byref(tc), ctypes.byref(td), ctypes.byref(cb))
+        if rc != 0:
+            raise RuntimeError("CPU baseline round trip failed")
+        return tc.value, td.value
+
+    nall = len(sample) // size
+    res = {}
+    for label, th, n, budget in (("all", threads, nall, 0.7 * seconds), ("one", 1, max(nall // 16, 1024), 0.3 * seconds)):
+        tc, td = run(n, th, 1)
+        passes = int(min(50, max(1, math.ceil(budget / max(tc + td, 1e-3)))))
+        tc, td = run(n, th, passes)
+        raw = float(n) * size * passes
+        res[label] = dict(rt=raw / (tc + td) / GIB, c=raw / tc / GIB, d=raw / td / GIB, n=n, passes=passes)
+    a, o = res["all"], res["one"]
+    return {
+        "value": round(a["rt"], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "sample": (f"{a['n']} x {size} B G1-long values (the first values of the GPU batch), "
+                   f"{a['passes']} timed round-trip passes after 1 warm-up, blocked partition over "
+                   f"{threads} threads; CPU: {cpu_model()}"),
+        "compress_gibs": round(a["c"], 3), "decompress_gibs": round(a["d"], 3),
+        "one_thread": {"value": round(o["rt"], 3), "compress_gibs": round(o["c"], 3),
+                       "decompress_gibs": round(o["d"], 3), "values": o["n"], "passes": o["passes"]},
+        "source": ("algorithm/lz4.cc LZ4_compress_limitedOutput + LZ4_decompress_safe_partial, compiled "
+                   "from the reference (oracle/_ref)" if kind == "reference" else
+                   "oracle/lz4_oracle.c restatement (reference build absent)"),
+    }
+
+
+def main() -> None:
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+
+    # torch first (plumbing: gloo barrier / max-over-ranks, torch.cuda.synchronize):
+    # loading it before libkdb_lz4.so keeps ONE HIP runtime in the process.
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    import kingdb_amd as K
+    from kingdb_amd import lz4 as L
+
+    K.set_device(local)
+    torch_sync = torch.cuda.is_available()
+    if torch_sync:
+        torch.cuda.set_device(local)
+
+    def sync_all():
+        L.lib().kdb_lz4_device_sync()
+        if torch_sync:
+            torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    n, size = args.values, args.size
+    stream = K.Stream()
+    first_piece = rank * ((n * size + 99) // 100)
+    batch = K.DeviceBatch.g1_long(n, size, first_piece=first_piece, stream=stream)
+    stream.sync()
+
+    for _ in range(args.warmup):
+        batch.compress(stream)
+        batch.decompress(stream)
+    stream.sync()
+
+    evs = [[K.Event() for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        batch.compress(stream)
+        evs[k][1].record(stream)
+        batch.decompress(stream)
+        evs[k][2].record(stream)
+    stream.sync()
+    sync_all()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    c_ms = float(np.mean([evs[k][0].elapsed_ms(evs[k][1]) for k in range(args.steps)]))
+    d_ms = float(np.mean([evs[k][1].elapsed_ms(evs[k][2]) for k in range(args.steps)]))
+
+    # correctness of what was timed (outside the timed region)
+    cst, dst = batch.status()
+    flen = batch.frame_lens().astype(np.int64)
+    ok = bool((cst == 0).all() and (dst == 0).all() and (batch.out_lens() == size).all())
+    if ok and not args.no_verify:
+        ok = bool(np.array_equal(batch.src.download(n * size), batch.out.download(n * size)))
+    if not ok:
+        raise SystemExit("bench: round trip is not bit-exact -- refusing to report a number")
+
+    raw = float(n) * size
+    frames = float(flen.sum())
+    alg_bytes = raw + frames  # per launch, compress and decompress alike
+    dom_name, dom_ms = ("lz4_compress_kernel<true>", c_ms) if c_ms >= d_ms else ("lz4_decompress_kernel<true>", d_ms)
+    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        pm = json.load(open(args.pmc))
+        if pm.get("values") == n and pm.get("size") == size and dom_name in pm.get("kernels", {}):
+            traffic = pm["kernels"][dom_name]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+
+    total_raw = raw * world * args.steps
+    value = total_raw / elapsed / GIB
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: G1-long (db_bench CompressibleString 0.5, LevelDB Random(301)), generated on device",
+        "config": {
+            "workload": f"{n} x {size} B values per GPU: CompressorLZ4 frame compress + frame decompress (round trip)",
+            "values_per_gpu": n, "value_bytes": size, "parallelism": f"dp{world} (independent shards, no collective)",
+            "ratio": round(frames / raw, 4),
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": dom_name,
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(dom_ms, 4),
+        },
+        "kernels_ms": {"compress": round(c_ms, 4), "decompress": round(d_ms, 4)},
+        "compress_gibs": round(raw / (c_ms * 1e-3) / GIB, 2),
+        "decompress_gibs": round(raw / (d_ms * 1e-3) / GIB, 2),
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ncpu = min(n, 131072)
+        sample = batch.src.download(ncpu * size)
+        line["cpu_baseline"] = cpu_baseline(sample, size, args.cpu_seconds)
+    batch.free()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -26,6 +26,24 @@
 
 namespace kdb_lz4 {
 
+#ifdef KDB_LZ4_STAMPS
+// Diagnostic build only (never the shipped .so): per-phase shader-clock sums.
+__device__ unsigned long long g_stamps[16];
+struct Stamps {
+  unsigned long long last, acc[12];
+  __device__ void start() { last = __builtin_amdgcn_s_memtime(); for (int i = 0; i < 12; ++i) acc[i] = 0; }
+  __device__ void mark(int i) { unsigned long long t = __builtin_amdgcn_s_memtime(); acc[i] += t - last; last = t; }
+  __device__ void count(int i) { acc[i] += 1; }
+  __device__ void flush() { if (__lane_id() == 0) for (int i = 0; i < 12; ++i) atomicAdd(&g_stamps[i], acc[i]); }
+};
+#define ST_MARK(i) st.mark(i)
+#define ST_COUNT(i) st.count(i)
+#else
+struct Stamps { __device__ void start() {} __device__ void flush() {} };
+#define ST_MARK(i) ((void)0)
+#define ST_COUNT(i) ((void)0)
+#endif
+
 // Position visited at iteration k of a search run started at s (lz4.cc:497-507):
 // p(0)=s, p(k+1)=p(k)+step(k), step(0)=1, step(k)=(63+k)>>6 for k>=1, i.e.
 // p(k) = s + 1 + sum_{t=64}^{62+k} floor(t/64) for k >= 1.
@@ -67,7 +85,7 @@ __device__ __forceinline__ void emit_bytes(const Sink& sk, int pos, const uint8_
 // Returns the block size or 0 (limitedOutput failure), like the reference.
 __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_base,
                               uint32_t head, uint32_t S, uint16_t* __restrict__ tab,
-                              const Sink& sk) {
+                              const Sink& sk, Stamps& st) {
   const uint32_t lane = lane_id();
   const int cap = sk.cap;
   int op = 0;
@@ -83,7 +101,9 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
       // ================= search (lz4.cc:494-527), 64 iterations per step
       uint32_t ip = 0, ref = 0;
       bool found = false;
+      ST_MARK(7);
       for (uint32_t kb = 0;; kb += 64u) {
+        ST_COUNT(8);
         const uint32_t k = kb + lane;
         const uint32_t pk = search_pos(s, k);
         const bool valid = search_pos(s, k + 1u) <= mflimit;      // lz4.cc:510
@@ -115,7 +135,9 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
         if (vm != ~0ull) break;              // ran past mflimit: last literals
         if ((same & ~mask_le(lane)) == 0) tab[h] = (uint16_t)pk;
       }
+      ST_MARK(1);
       if (!found) break;
+      ST_COUNT(9);
 
       // ================= catch up (lz4.cc:531)
       for (;;) {
@@ -128,6 +150,7 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
         if (c < 64u) break;
       }
 
+      ST_MARK(2);
       // ================= literal length + literals (lz4.cc:535-550)
       int tok_pos = op++;
       uint32_t token;
@@ -144,6 +167,7 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
         op += (int)lit;
       }
 
+      ST_MARK(3);
       for (;;) {  // _next_match (lz4.cc:552)
         // offset (lz4.cc:554)
         const uint32_t off = ip - ref;
@@ -170,6 +194,7 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
           token += ml;
         }
         if (lane == 0) sk.put(tok_pos, token);
+        ST_MARK(4);
         anchor = ip;
         if (ip > mflimit) goto last_literals;                      // lz4.cc:597
 
@@ -184,8 +209,10 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
           ref = r2;
           tok_pos = op++;
           token = 0;
+          ST_MARK(5);
           continue;                                                  // goto _next_match
         }
+        ST_MARK(5);
         break;
       }
       s = ip + 1u;                                                   // lz4.cc:623
@@ -193,6 +220,7 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
   }
 
 last_literals:
+  ST_MARK(7);
   {  // lz4.cc:627-637
     const uint32_t run = S - anchor;
     if ((int64_t)op + run + 1 + (run + 255u - kRunMask) / 255u > (int64_t)(uint32_t)cap) return 0;
@@ -208,6 +236,7 @@ last_literals:
     op += (int)run;
   }
 #undef RD32
+  ST_MARK(6);
   return op;
 }
 
@@ -236,6 +265,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     if (lane == 0) { ret[v] = kUnsupported; if (kFrame) frame_len[v] = 0; }
     return;
   }
+  Stamps st;
+  st.start();
   const uint32_t head = stage_to_lds(g, S, s_in);
   {  // zero the table (lz4.cc:669)
     uint4* t4 = reinterpret_cast<uint4*>(tab);
@@ -243,16 +274,18 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) t4[i] = z;
   }
   __syncthreads();
+  ST_MARK(0);
 
   const uint8_t* in = s_in + head;
   if (!kFrame) {
     Sink sk{o, (int)dst_cap[v]};
-    const int r = compress_block(in, s_in, head, S, tab, sk);
+    const int r = compress_block(in, s_in, head, S, tab, sk, st);
     if (lane == 0) ret[v] = r;
+    st.flush();
   } else {
     const uint32_t bound = compress_bound(S);
     Sink sk{o + 8, (int)bound};
-    const int r = compress_block(in, s_in, head, S, tab, sk);
+    const int r = compress_block(in, s_in, head, S, tab, sk, st);
     // compressor.cc:31-59
     uint32_t stored, flen;
     if (r <= 0) {
@@ -272,6 +305,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       o[lane] = (uint8_t)(w >> (8u * (lane & 3u)));
     }
     if (lane == 0) { ret[v] = 0; frame_len[v] = flen; }
+    ST_MARK(10);
+    st.flush();
   }
 }
 
@@ -286,6 +321,16 @@ template __global__ void lz4_compress_kernel<true>(const uint8_t*, const uint64_
 size_t compress_lds_bytes(uint32_t max_len) {
   return kTableBytes + (((size_t)max_len + 15u) & ~(size_t)15u) + 48u;
 }
+
+#ifdef KDB_LZ4_STAMPS
+extern "C" int kdb_lz4_stamps_read(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+}
+extern "C" int kdb_lz4_stamps_reset() {
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                            const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,

@@ -360,3 +360,77 @@ void orc_g1_pieces(uint32_t seed, uint64_t npieces, uint8_t* out) {
     memcpy(out + p * 100 + 50, raw, 50);
   }
 }
+
+/* ---- CPU baseline harness (bench.py cpu_baseline leg, kind "port") -------
+ * Same protocol as oracle/ref_shim.cc:ref_bench_roundtrip, over this
+ * restatement: blocked partition over pthreads, one warm-up pass, `passes`
+ * timed passes, compress and decompress phases timed separately. */
+#include <pthread.h>
+#include <stdlib.h>
+#include <time.h>
+
+typedef struct {
+  const uint8_t* src; uint8_t* blocks; int* blen; uint8_t* out;
+  int lo, hi, size, bound, comp, bad;
+} orc_job;
+
+static void* orc_bench_worker(void* p) {
+  orc_job* j = (orc_job*)p;
+  for (int i = j->lo; i < j->hi; i++) {
+    if (j->comp) {
+      j->blen[i] = orc_compress_limited(j->src + (size_t)i * j->size, j->blocks + (size_t)i * j->bound,
+                                        j->size, j->bound);
+    } else {
+      int r = orc_decompress_safe_partial(j->blocks + (size_t)i * j->bound, j->out + (size_t)i * j->size,
+                                          j->blen[i], j->size, j->size);
+      if (r != j->size) j->bad = 1;
+    }
+  }
+  return NULL;
+}
+
+static double orc_now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int orc_bench_phase(orc_job* jobs, int threads, int comp) {
+  pthread_t th[256];
+  int bad = 0;
+  for (int t = 0; t < threads; t++) { jobs[t].comp = comp; pthread_create(&th[t], NULL, orc_bench_worker, &jobs[t]); }
+  for (int t = 0; t < threads; t++) { pthread_join(th[t], NULL); bad |= jobs[t].bad; }
+  return bad;
+}
+
+int orc_bench_roundtrip(const uint8_t* src, int n, int size, int threads, int passes,
+                        double* t_compress, double* t_decompress, uint64_t* comp_bytes) {
+  if (threads > 256) threads = 256;
+  const int bound = orc_compress_bound(size) + 8;
+  uint8_t* blocks = (uint8_t*)malloc((size_t)n * bound);
+  int* blen = (int*)malloc(sizeof(int) * (size_t)n);
+  uint8_t* out = (uint8_t*)malloc((size_t)n * size + 64);
+  orc_job jobs[256];
+  for (int t = 0; t < threads; t++) {
+    orc_job j = {src, blocks, blen, out, (int)((int64_t)n * t / threads), (int)((int64_t)n * (t + 1) / threads),
+                 size, bound - 8, 0, 0};
+    jobs[t] = j;
+  }
+  int bad = orc_bench_phase(jobs, threads, 1) | orc_bench_phase(jobs, threads, 0);
+  double tc = 0, td = 0;
+  for (int p = 0; p < passes; p++) {
+    double a = orc_now();
+    bad |= orc_bench_phase(jobs, threads, 1);
+    double b = orc_now();
+    bad |= orc_bench_phase(jobs, threads, 0);
+    double c = orc_now();
+    tc += b - a;
+    td += c - b;
+  }
+  uint64_t cb = 0;
+  for (int i = 0; i < n; i++) cb += (uint64_t)blen[i];
+  *t_compress = tc; *t_decompress = td; *comp_bytes = cb;
+  if (memcmp(out, src, (size_t)n * size) != 0) bad = 1;
+  free(blocks); free(blen); free(out);
+  return bad ? -1 : 0;
+}

@@ -108,3 +108,57 @@ void ref_gen_g3(char* out, int size, int count) {
 }
 
 }  // extern "C"
+
+// ---- CPU baseline harness (bench.py cpu_baseline leg, kind "reference") ----
+// Times the reference's own block codec -- LZ4_compress_limitedOutput with a
+// bound-sized slot, then LZ4_decompress_safe_partial(target = max = size) --
+// over n values of `size` bytes with `threads` std::threads, each owning a
+// contiguous (blocked) range of values.  One untimed warm-up pass, then
+// `passes` timed passes; compress and decompress phases are timed separately
+// (steady_clock).  Returns 0, or -1 if any value fails to round-trip.
+#include <chrono>
+#include <thread>
+extern "C" int ref_bench_roundtrip(const char* src, int n, int size, int threads, int passes,
+                                   double* t_compress, double* t_decompress, uint64_t* comp_bytes) {
+  const int bound = LZ4_compressBound(size);
+  std::vector<char> blocks((size_t)n * bound);
+  std::vector<int> blen(n);
+  std::vector<char> out((size_t)n * size);
+  int bad = 0;
+  auto run = [&](bool comp) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+      th.emplace_back([&, t]() {
+        int lo = (int)((int64_t)n * t / threads), hi = (int)((int64_t)n * (t + 1) / threads);
+        for (int i = lo; i < hi; i++) {
+          if (comp) {
+            blen[i] = LZ4_compress_limitedOutput(src + (size_t)i * size, &blocks[(size_t)i * bound], size, bound);
+          } else {
+            int r = LZ4_decompress_safe_partial(&blocks[(size_t)i * bound], &out[(size_t)i * size], blen[i], size, size);
+            if (r != size) bad = 1;
+          }
+        }
+      });
+    }
+    for (auto& x : th) x.join();
+  };
+  run(true);
+  run(false);
+  double tc = 0, td = 0;
+  for (int p = 0; p < passes; p++) {
+    auto a = std::chrono::steady_clock::now();
+    run(true);
+    auto b = std::chrono::steady_clock::now();
+    run(false);
+    auto c = std::chrono::steady_clock::now();
+    tc += std::chrono::duration<double>(b - a).count();
+    td += std::chrono::duration<double>(c - b).count();
+  }
+  uint64_t cb = 0;
+  for (int i = 0; i < n; i++) cb += (uint64_t)blen[i];
+  *t_compress = tc;
+  *t_decompress = td;
+  *comp_bytes = cb;
+  if (memcmp(out.data(), src, (size_t)n * size) != 0) bad = 1;
+  return bad ? -1 : 0;
+}
