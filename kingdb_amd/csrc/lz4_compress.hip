@@ -5,8 +5,14 @@
 // (lz4.cc:431-641), fused with CompressorLZ4::Compress's frame epilogue
 // (algorithm/compressor.cc:26-59).  Output is byte-identical to the reference.
 //
-// One wavefront per value.  LDS per workgroup: the byU16 hash table (8192 x u16,
-// zeroed per value -- lz4.cc:669's zeroed context) + the value staged from HBM.
+// Persistent launch: one wavefront (workgroup of 64) per resident slot walks
+// the batch with a grid stride.  LDS per workgroup: the byU16 hash table
+// (8192 x u16), the staged value and the block being assembled (flushed to HBM
+// with 16-byte stores).  For launches whose values are all <= 4 KiB the table
+// carries a 4-bit generation tag beside each 12-bit position, so it is cleared
+// once per 15 values instead of per value (a stale tag reads as the zeroed
+// slot, position 0 -- lz4.cc:669 semantics), and the next value is prefetched
+// into registers while the current one is parsed.
 //
 // The greedy parse is sequential by definition; what is parallel is:
 //  * the search loop (lz4.cc:494-527): the positions it visits from a start
@@ -19,30 +25,13 @@
 //    matching lane ends the chunk; only puts of lanes up to it are committed
 //    (the last lane of each group writes), exactly the table state the
 //    sequential loop would leave;
-//  * LZ4_count (lz4.cc:412-428) and the catch-up loop (lz4.cc:531): 64-byte
-//    compares, ballot, first-mismatch;
+//  * the catch-up loop (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued
+//    together: the match length after catching up c bytes is c + the length
+//    measured from the original position, so neither waits for the other;
 //  * literal copies and length-byte runs.
 #include "lz4_device.h"
 
 namespace kdb_lz4 {
-
-#ifdef KDB_LZ4_STAMPS
-// Diagnostic build only (never the shipped .so): per-phase shader-clock sums.
-__device__ unsigned long long g_stamps[16];
-struct Stamps {
-  unsigned long long last, acc[12];
-  __device__ void start() { last = __builtin_amdgcn_s_memtime(); for (int i = 0; i < 12; ++i) acc[i] = 0; }
-  __device__ void mark(int i) { unsigned long long t = __builtin_amdgcn_s_memtime(); acc[i] += t - last; last = t; }
-  __device__ void count(int i) { acc[i] += 1; }
-  __device__ void flush() { if (__lane_id() == 0) for (int i = 0; i < 12; ++i) atomicAdd(&g_stamps[i], acc[i]); }
-};
-#define ST_MARK(i) st.mark(i)
-#define ST_COUNT(i) st.count(i)
-#else
-struct Stamps { __device__ void start() {} __device__ void flush() {} };
-#define ST_MARK(i) ((void)0)
-#define ST_COUNT(i) ((void)0)
-#endif
 
 // Position visited at iteration k of a search run started at s (lz4.cc:497-507):
 // p(0)=s, p(k+1)=p(k)+step(k), step(0)=1, step(k)=(63+k)>>6 for k>=1, i.e.
@@ -52,42 +41,74 @@ __device__ __forceinline__ uint32_t search_pos(uint32_t s, uint32_t k) {
   const uint32_t nn = 62u + k, q = nn >> 6, r = nn & 63u;
   return s + 1u + 32u * q * (q - 1u) + q * (r + 1u);
 }
+__device__ __forceinline__ uint32_t search_step(uint32_t k) { return k == 0 ? 1u : (63u + k) >> 6; }
 
 __device__ __forceinline__ uint32_t hash16(uint32_t seq) { return (seq * 2654435761u) >> 19; }
 
-// Output sink: global bytes at o[0..cap); never writes at or past cap (the
-// reference may, on limitedOutput failures -- the return value is what parity
-// is about, see oracle/lz4_oracle.c).
-struct Sink {
-  uint8_t* o;
-  int cap;
-  __device__ __forceinline__ void put(int pos, uint32_t b) const {
-    if (pos >= 0 && pos < cap) o[pos] = (uint8_t)b;
+// The byU16 table.  kTagged: entry = gen << 12 | pos (values <= 4 KiB, so
+// positions < 4096); an entry of another generation is an empty slot (0).
+template <bool kTagged>
+struct Table {
+  uint16_t* t;
+  uint32_t gen;
+  __device__ __forceinline__ uint32_t get(uint32_t h) const {
+    const uint32_t e = t[h];
+    if (kTagged) return (e >> 12) == gen ? (e & 0xfffu) : 0u;
+    return e;
+  }
+  __device__ __forceinline__ void put(uint32_t h, uint32_t p) const {
+    t[h] = (uint16_t)(kTagged ? ((gen << 12) | p) : p);
   }
 };
 
-// Emits `run` as a length continuation (nb 255s + remainder) at o[pos..];
-// returns the number of bytes written.  Wave-cooperative.
-__device__ __forceinline__ int emit_len(const Sink& sk, int pos, uint32_t run) {
-  const uint32_t nb = run / 255u, rem = run - nb * 255u;
-  for (uint32_t i = lane_id(); i <= nb; i += 64u) sk.put(pos + (int)i, i < nb ? 255u : rem);
-  return (int)nb + 1;
+// Output: the block is assembled in LDS (out[0..out_cap)) and flushed to HBM
+// once complete.  kGuard (LZ4_compress_limitedOutput with a caller cap below
+// the bound): never write at or past out_cap -- the reference may, on
+// limitedOutput failures; the return value is what parity is about (see
+// oracle/lz4_oracle.c).  Without kGuard the cap is the bound, which the block
+// never exceeds.
+template <bool kGuard>
+__device__ __forceinline__ void put8(uint8_t* out, int out_cap, int pos, uint32_t b) {
+  if (!kGuard || (uint32_t)pos < (uint32_t)out_cap) out[pos] = (uint8_t)b;
 }
 
-// Copies n input bytes (value position a..a+n) to o[pos..pos+n).
-__device__ __forceinline__ void emit_bytes(const Sink& sk, int pos, const uint8_t* in,
-                                           uint32_t a, uint32_t n) {
-  for (uint32_t i = lane_id(); i < n; i += 64u) sk.put(pos + (int)i, in[a + i]);
+// Lanes 0..nb write a length continuation (nb 255s then `rem`) at out[pos..].
+template <bool kGuard>
+__device__ __forceinline__ void put_len(uint8_t* out, int out_cap, int pos, uint32_t nb, uint32_t rem) {
+  const uint32_t lane = lane_id();
+#pragma unroll 1
+  for (uint32_t i = 0; i <= nb; i += 64u) {
+    const uint32_t j = i + lane;
+    if (j <= nb) put8<kGuard>(out, out_cap, pos + (int)j, j < nb ? 255u : rem);
+  }
+}
+
+// out[pos .. pos+n) = in[a .. a+n), 64 bytes per step.
+template <bool kGuard>
+__device__ __forceinline__ void put_bytes(uint8_t* out, int out_cap, int pos, const uint8_t* in, uint32_t a,
+                                          uint32_t n) {
+#ifdef KDB_ABL_NO_EMIT
+  return;
+#endif
+  const uint32_t lane = lane_id();
+#pragma unroll 1
+  for (uint32_t i = 0; i < n; i += 64u) {
+    const uint32_t j = i + lane;
+    const uint32_t b = in[a + j];
+    if (j < n) put8<kGuard>(out, out_cap, pos + (int)j, b);
+  }
 }
 
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
-// in[i] (caller passes the head-adjusted base), readable 8 bytes past S.
-// Returns the block size or 0 (limitedOutput failure), like the reference.
-__device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_base,
-                              uint32_t head, uint32_t S, uint16_t* __restrict__ tab,
-                              const Sink& sk, Stamps& st) {
+// in[i]; in_base/head: the 16B-aligned buffer and the offset of byte 0; the
+// buffer is readable well past S, so reads are issued unconditionally and
+// masked afterwards.  Returns the block size or 0 (limitedOutput failure,
+// checked against `cap` at the reference's check points), like the reference.
+template <bool kTagged, bool kGuard>
+__device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_base, uint32_t head,
+                              uint32_t S, const Table<kTagged>& tab, uint8_t* __restrict__ out, int out_cap,
+                              int cap) {
   const uint32_t lane = lane_id();
-  const int cap = sk.cap;
   int op = 0;
   uint32_t anchor = 0;
 #define RD32(p) lds_rd32(in_base, head + (p))
@@ -95,30 +116,31 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
   if (S >= kMinLength) {                                    // lz4.cc:483
     const uint32_t mflimit = S - kMfLimit;
     const uint32_t matchlimit = S - kLastLiterals;
-    // lz4.cc:486: put(0) -- a no-op on the zeroed table.
+    // lz4.cc:486: put(0) stores position 0 -- what an empty slot already reads as.
     uint32_t s = 1;                                         // lz4.cc:487
     for (;;) {
       // ================= search (lz4.cc:494-527), 64 iterations per step
       uint32_t ip = 0, ref = 0;
       bool found = false;
-      ST_MARK(7);
+#pragma unroll 1
       for (uint32_t kb = 0;; kb += 64u) {
-        ST_COUNT(8);
         const uint32_t k = kb + lane;
         const uint32_t pk = search_pos(s, k);
-        const bool valid = search_pos(s, k + 1u) <= mflimit;      // lz4.cc:510
-        const uint32_t seq = valid ? RD32(pk) : 0u;
+        const bool valid = pk + search_step(k) <= mflimit;         // lz4.cc:510
+        const uint32_t seq = RD32(pk);
         const uint32_t h = hash16(seq);
-        const uint32_t told = valid ? (uint32_t)tab[h] : 0u;
+        const uint32_t told = tab.get(h);
         const uint64_t vm = __ballot(valid);
         // lanes of this chunk whose iteration hashes to the same slot
-        uint64_t same = vm;
+        uint32_t lo = ~0u, hi = ~0u;
 #pragma unroll
         for (int b = 0; b < 13; ++b) {
-          const uint32_t bit = (h >> b) & 1u;
-          const uint64_t m = __ballot(bit);
-          same &= bit ? m : ~m;
+          const uint32_t t = (uint32_t)((int32_t)(h << (31 - b)) >> 31);   // 0 or ~0
+          const uint64_t m = __ballot(t != 0u);
+          lo &= ~(t ^ (uint32_t)m);
+          hi &= ~(t ^ (uint32_t)(m >> 32));
         }
+        const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;
         const uint64_t below = same & mask_lt(lane);
         const uint32_t refk = below ? search_pos(s, kb + 63u - (uint32_t)__builtin_clzll(below)) : told;
         const bool match = valid && RD32(refk) == seq;           // lz4.cc:527
@@ -126,93 +148,95 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
           const uint64_t later = same & ~mask_le(lane) & mask_le(ks);
-          if (valid && lane <= ks && later == 0) tab[h] = (uint16_t)pk;   // lz4.cc:526
+          if (valid && lane <= ks && later == 0) tab.put(h, pk);   // lz4.cc:526
           ip = readlane(pk, ks);
           ref = readlane(refk, ks);
           found = true;
           break;
         }
         if (vm != ~0ull) break;              // ran past mflimit: last literals
-        if ((same & ~mask_le(lane)) == 0) tab[h] = (uint16_t)pk;
+        if ((same & ~mask_le(lane)) == 0) tab.put(h, pk);
       }
-      ST_MARK(1);
       if (!found) break;
-      ST_COUNT(9);
 
-      // ================= catch up (lz4.cc:531)
-      for (;;) {
-        const uint32_t lim = min(ip - anchor, ref);
-        if (lim == 0) break;
-        const bool eq = lane < lim && in[ip - 1u - lane] == in[ref - 1u - lane];
-        const uint32_t c = first_zero(__ballot(eq));
-        ip -= c;
-        ref -= c;
-        if (c < 64u) break;
-      }
-
-      ST_MARK(2);
-      // ================= literal length + literals (lz4.cc:535-550)
-      int tok_pos = op++;
-      uint32_t token;
-      {
-        const uint32_t lit = ip - anchor;
-        if ((int64_t)op + lit + (2 + 1 + kLastLiterals) + lit / 255u > (int64_t)cap) return 0;
-        if (lit >= kRunMask) {
-          token = kRunMask << 4;
-          op += emit_len(sk, op, lit - kRunMask);
-        } else {
-          token = lit << 4;
-        }
-        emit_bytes(sk, op, in, anchor, lit);
-        op += (int)lit;
-      }
-
-      ST_MARK(3);
-      for (;;) {  // _next_match (lz4.cc:552)
-        // offset (lz4.cc:554)
-        const uint32_t off = ip - ref;
-        if (lane < 2u) sk.put(op + (int)lane, lane ? (off >> 8) : (off & 255u));
-        op += 2;
-        // match length (lz4.cc:557-592)
-        uint32_t ml = 0;
+      bool catchup = true;
+#pragma unroll 1
+      for (;;) {  // one sequence per iteration; `continue` = _next_match with no literals
+        // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
+        uint32_t c, ml;
         {
-          const uint32_t a = ip + kMinMatch, b = ref + kMinMatch;
-          for (;;) {
-            const uint32_t rem = matchlimit - (a + ml);
-            const bool eq = lane < rem && in[a + ml + lane] == in[b + ml + lane];
-            const uint32_t c = first_zero(__ballot(eq));
-            ml += c;
-            if (c < 64u) break;
+          const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
+          const uint32_t rem = matchlimit - (ip + kMinMatch);
+          const uint32_t a0 = in[ip - 1u - lane], b0 = in[ref - 1u - lane];
+          const uint32_t a1 = in[ip + kMinMatch + lane], b1 = in[ref + kMinMatch + lane];
+          c = first_zero(__ballot(lane < lim && a0 == b0));      // <= lim
+          ml = first_zero(__ballot(lane < rem && a1 == b1));     // <= rem
+          if (c == 64u) {
+#pragma unroll 1
+            for (;;) {
+              const uint32_t x = in[ip - c - 1u - lane], y = in[ref - c - 1u - lane];
+              const uint32_t d = first_zero(__ballot(lane < lim - c && x == y));
+              c += d;
+              if (d < 64u) break;
+            }
+          }
+          if (ml == 64u) {
+#pragma unroll 1
+            for (;;) {
+              const uint32_t x = in[ip + kMinMatch + ml + lane], y = in[ref + kMinMatch + ml + lane];
+              const uint32_t d = first_zero(__ballot(lane < rem - ml && x == y));
+              ml += d;
+              if (d < 64u) break;
+            }
           }
         }
-        ip += kMinMatch + ml;
+        const uint32_t ip_end = ip + kMinMatch + ml;  // independent of the catch-up
+        ip -= c;
+        ref -= c;
+        ml += c;
+
+        // ======== token + literals (lz4.cc:535-550), offset (554), match length (580-592)
+        const uint32_t lit = ip - anchor;
+        const int tok_pos = op;
+        op += 1;
+        if ((int64_t)op + lit + (2 + 1 + kLastLiterals) + lit / 255u > (int64_t)cap) return 0;
+        uint32_t token = (lit >= kRunMask ? kRunMask : lit) << 4;
+        if (lit >= kRunMask) {
+          const uint32_t nb = (lit - kRunMask) / 255u;
+          put_len<kGuard>(out, out_cap, op, nb, lit - kRunMask - 255u * nb);
+          op += (int)nb + 1;
+        }
+        put_bytes<kGuard>(out, out_cap, op, in, anchor, lit);
+        op += (int)lit;
+        const uint32_t off = ip - ref;
+        if (lane < 2u) put8<kGuard>(out, out_cap, op + (int)lane, lane ? (off >> 8) : (off & 255u));
+        op += 2;
         if (ml >= kMlMask) {
           if ((int64_t)op + (1 + kLastLiterals) + (ml >> 8) > (int64_t)cap) return 0;
           token += kMlMask;
-          op += emit_len(sk, op, ml - kMlMask);
+          const uint32_t nb = (ml - kMlMask) / 255u;
+          put_len<kGuard>(out, out_cap, op, nb, ml - kMlMask - 255u * nb);
+          op += (int)nb + 1;
         } else {
           token += ml;
         }
-        if (lane == 0) sk.put(tok_pos, token);
-        ST_MARK(4);
+        if (lane == 0) put8<kGuard>(out, out_cap, tok_pos, token);
+        ip = ip_end;
         anchor = ip;
         if (ip > mflimit) goto last_literals;                      // lz4.cc:597
 
-        // fill table + test next position (lz4.cc:600-624)
-        const uint32_t hm2 = hash16(RD32(ip - 2u));
-        if (lane == 0) tab[hm2] = (uint16_t)(ip - 2u);
+        // ======== fill table + test next position (lz4.cc:600-624)
+        const uint32_t sm2 = RD32(ip - 2u);
         const uint32_t sq = RD32(ip);
         const uint32_t hh = hash16(sq);
-        const uint32_t r2 = uni(tab[hh]);
-        if (lane == 0) tab[hh] = (uint16_t)ip;
+        if (lane == 0) tab.put(hash16(sm2), ip - 2u);
+        const uint32_t r2 = uni(tab.get(hh));
+        if (lane == 0) tab.put(hh, ip);
         if (r2 + kMaxDistance >= ip && RD32(r2) == sq) {
           ref = r2;
-          tok_pos = op++;
-          token = 0;
-          ST_MARK(5);
+          catchup = false;
           continue;                                                  // goto _next_match
         }
-        ST_MARK(5);
         break;
       }
       s = ip + 1u;                                                   // lz4.cc:623
@@ -220,31 +244,39 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
   }
 
 last_literals:
-  ST_MARK(7);
   {  // lz4.cc:627-637
     const uint32_t run = S - anchor;
     if ((int64_t)op + run + 1 + (run + 255u - kRunMask) / 255u > (int64_t)(uint32_t)cap) return 0;
+    if (lane == 0) put8<kGuard>(out, out_cap, op, (run >= kRunMask ? kRunMask : run) << 4);
+    op += 1;
     if (run >= kRunMask) {
-      if (lane == 0) sk.put(op, kRunMask << 4);
-      op += 1;
-      op += emit_len(sk, op, run - kRunMask);
-    } else {
-      if (lane == 0) sk.put(op, run << 4);
-      op += 1;
+      const uint32_t nb = (run - kRunMask) / 255u;
+      put_len<kGuard>(out, out_cap, op, nb, run - kRunMask - 255u * nb);
+      op += (int)nb + 1;
     }
-    emit_bytes(sk, op, in, anchor, run);
+    put_bytes<kGuard>(out, out_cap, op, in, anchor, run);
     op += (int)run;
   }
 #undef RD32
-  ST_MARK(6);
   return op;
+}
+
+constexpr uint32_t kSmallMax = 4096u;     // tagged table + register prefetch
+constexpr uint32_t kPrefetch = 5u;        // 16-byte loads per lane: (15 + 4096 + 15) / 16 / 64 < 5
+
+// Staged-input region: value bytes + 16-byte-load slack; the register prefetch
+// of small launches writes kPrefetch whole KiB.
+__host__ __device__ __forceinline__ uint32_t in_region_bytes(bool small, uint32_t in_cap) {
+  const uint32_t a = ((in_cap + 15u) & ~15u) + 48u;
+  const uint32_t b = small ? kPrefetch * 64u * 16u + 16u : 0u;
+  return a > b ? a : b;
 }
 
 // kFrame = false: LZ4_compress_limitedOutput per value; ret[v] = size or 0,
 //   dst slot capacity = cap[v].
 // kFrame = true : CompressorLZ4::Compress per value; the slot must hold
 //   8 + compress_bound(S) bytes; frame_len[v] = frame bytes, ret[v] = 0 or -1.
-template <bool kFrame>
+template <bool kFrame, bool kSmall>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t in_cap,
@@ -252,100 +284,150 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
     int32_t* __restrict__ ret) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t v = blockIdx.x;
-  if (v >= n) return;
   const uint32_t lane = lane_id();
-  uint16_t* tab = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
   uint8_t* s_in = smem + kTableBytes;
+  const uint32_t in_bytes = in_region_bytes(kSmall, in_cap);
+  uint8_t* s_out = s_in + in_bytes;       // [8-byte frame header][block]
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
 
-  const uint32_t S = uni(src_len[v]);
-  const uint8_t* g = src + src_off[v];
-  uint8_t* o = dst + dst_off[v];
-  if (S > in_cap || S >= k64KLimit) {             // byU32 sizes: not this kernel
-    if (lane == 0) { ret[v] = kUnsupported; if (kFrame) frame_len[v] = 0; }
-    return;
+  Table<kSmall> tab{tab16, 1u};
+  if (kSmall) {
+    for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
   }
-  Stamps st;
-  st.start();
-  const uint32_t head = stage_to_lds(g, S, s_in);
-  {  // zero the table (lz4.cc:669)
-    uint4* t4 = reinterpret_cast<uint4*>(tab);
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) t4[i] = z;
-  }
-  __syncthreads();
-  ST_MARK(0);
-
-  const uint8_t* in = s_in + head;
-  if (!kFrame) {
-    Sink sk{o, (int)dst_cap[v]};
-    const int r = compress_block(in, s_in, head, S, tab, sk, st);
-    if (lane == 0) ret[v] = r;
-    st.flush();
-  } else {
-    const uint32_t bound = compress_bound(S);
-    Sink sk{o + 8, (int)bound};
-    const int r = compress_block(in, s_in, head, S, tab, sk, st);
-    // compressor.cc:31-59
-    uint32_t stored, flen;
-    if (r <= 0) {
-      if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
-      return;
+  // register prefetch (kSmall): the next value's 16-byte chunks, lane-strided
+  uint4 pf[kPrefetch];
+  uint32_t v = blockIdx.x;
+  auto prefetch = [&](uint32_t w) {
+    if (w < n) {
+      const uint8_t* gp = src + src_off[w];
+      const uint32_t hd = (uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u);
+      const uint4* base = reinterpret_cast<const uint4*>(gp - hd);
+      const uint32_t chunks = (hd + min(src_len[w], kSmallMax) + 15u) >> 4;
+#pragma unroll
+      for (uint32_t i = 0; i < kPrefetch; ++i) {
+        const uint32_t c = lane + 64u * i;
+        pf[i] = c < chunks ? base[c] : z4;
+      }
     }
-    if ((uint32_t)r > S) {                    // raw fallback (compressor.cc:40-48)
-      emit_bytes(Sink{o + 8, (int)S}, 0, in, 0, S);
-      stored = 0;
-      flen = S + 8u;
+  };
+  if (kSmall) prefetch(v);
+
+  for (; v < n; v += gridDim.x) {
+    const uint32_t S = uni(src_len[v]);
+    const uint8_t* g = src + src_off[v];
+    uint8_t* o = dst + dst_off[v];
+    if (S > in_cap || S >= k64KLimit) {             // byU32 sizes: not this kernel
+      if (lane == 0) { ret[v] = kUnsupported; if (kFrame) frame_len[v] = 0; }
+      if (kSmall) prefetch(v + gridDim.x);
+      continue;
+    }
+    uint32_t head;
+    if (kSmall) {
+      head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+#pragma unroll
+      for (uint32_t i = 0; i < kPrefetch; ++i) reinterpret_cast<uint4*>(s_in)[lane + 64u * i] = pf[i];
+      prefetch(v + gridDim.x);       // the next value's loads fly while this one is parsed
     } else {
-      stored = (uint32_t)r + 8u;
-      flen = stored;
+      head = stage_to_lds(g, S, s_in);
+#ifndef KDB_ABL_NO_ZERO
+      for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
+#endif
     }
-    if (lane < 8u) {
-      const uint32_t w = lane < 4u ? stored : S;
-      o[lane] = (uint8_t)(w >> (8u * (lane & 3u)));
+    __syncthreads();
+
+    const uint8_t* in = s_in + head;
+    const uint32_t bound = compress_bound(S);
+    if (!kFrame) {
+      const uint32_t cap = uni(dst_cap[v]);
+      // the block never needs more than `bound` bytes; a larger cap changes nothing
+      const int r = cap < bound
+                        ? compress_block<kSmall, true>(in, s_in, head, S, tab, s_out + 8, (int)cap, (int)cap)
+                        : compress_block<kSmall, false>(in, s_in, head, S, tab, s_out + 8, (int)bound, (int)cap);
+      if (r > 0) flush_lds_to_global(o, s_out, 8, (uint32_t)r);
+      if (lane == 0) ret[v] = r;
+    } else {
+      const int r = compress_block<kSmall, false>(in, s_in, head, S, tab, s_out + 8, (int)bound, (int)bound);
+      if (r <= 0) {                              // compressor.cc:31-34
+        if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
+      } else {
+        const bool raw = (uint32_t)r > S;        // raw fallback (compressor.cc:40-48)
+        const uint32_t stored = raw ? 0u : (uint32_t)r + 8u;
+        const uint32_t flen = raw ? S + 8u : stored;
+        if (lane < 8u) {                         // compressor.cc:53-54
+          const uint32_t w = lane < 4u ? stored : S;
+          s_out[lane] = (uint8_t)(w >> (8u * (lane & 3u)));
+        }
+        if (raw) {
+          flush_lds_to_global(o, s_out, 0, 8u);
+          flush_lds_to_global(o + 8, s_in, head, S);
+        } else {
+          flush_lds_to_global(o, s_out, 0, flen);
+        }
+        if (lane == 0) { ret[v] = 0; frame_len[v] = flen; }
+      }
     }
-    if (lane == 0) { ret[v] = 0; frame_len[v] = flen; }
-    ST_MARK(10);
-    st.flush();
+    if (kSmall) {
+      if (++tab.gen == 16u) {                    // tags exhausted: clear (lz4.cc:669)
+        tab.gen = 1u;
+#ifndef KDB_ABL_NO_ZERO
+        for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
+#endif
+      }
+    }
+    __syncthreads();
   }
 }
-
-template __global__ void lz4_compress_kernel<false>(const uint8_t*, const uint64_t*, const uint32_t*,
-                                                    uint32_t, uint32_t, uint8_t*, const uint64_t*,
-                                                    const uint32_t*, uint32_t*, int32_t*);
-template __global__ void lz4_compress_kernel<true>(const uint8_t*, const uint64_t*, const uint32_t*,
-                                                   uint32_t, uint32_t, uint8_t*, const uint64_t*,
-                                                   const uint32_t*, uint32_t*, int32_t*);
 
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
-  return kTableBytes + (((size_t)max_len + 15u) & ~(size_t)15u) + 48u;
+  const bool small = max_len <= kSmallMax;
+  const uint32_t m = small ? kSmallMax : max_len;
+  const size_t in_bytes = in_region_bytes(small, m);
+  const size_t out_bytes = ((8u + (size_t)compress_bound(m) + 15u) & ~(size_t)15u) + 16u;
+  return kTableBytes + in_bytes + out_bytes;
 }
 
-#ifdef KDB_LZ4_STAMPS
-extern "C" int kdb_lz4_stamps_read(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16) == hipSuccess ? 0 : -2;
+template <bool F, bool Sm>
+static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
+                             const uint32_t* src_len, uint32_t n, uint32_t in_cap, uint8_t* dst,
+                             const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
+                             int32_t* ret) {
+  auto kern = lz4_compress_kernel<F, Sm>;
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  const uint64_t slots = (uint64_t)per_cu * (uint64_t)cus;
+  const uint32_t grid = (uint32_t)(n < slots ? n : slots);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, in_cap, dst, dst_off,
+                     dst_cap, frame_len, ret);
+  return hipGetLastError();
 }
-extern "C" int kdb_lz4_stamps_reset() {
-  unsigned long long z[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) == hipSuccess ? 0 : -2;
-}
-#endif
 
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                            const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret) {
   if (n == 0) return hipSuccess;
-  const size_t lds = compress_lds_bytes(max_len);
+  const bool small = max_len <= kSmallMax;
+  const uint32_t in_cap = small ? kSmallMax : max_len;
+  size_t lds = compress_lds_bytes(max_len);
+#ifdef KDB_ABL_OCC
+  lds = 163840 / KDB_ABL_OCC;   // diagnostic: force KDB_ABL_OCC workgroups per CU
+#endif
   if (frame) {
-    hipLaunchKernelGGL(lz4_compress_kernel<true>, dim3(n), dim3(64), lds, st, src, src_off, src_len,
-                       n, max_len, dst, dst_off, dst_cap, frame_len, ret);
-  } else {
-    hipLaunchKernelGGL(lz4_compress_kernel<false>, dim3(n), dim3(64), lds, st, src, src_off,
-                       src_len, n, max_len, dst, dst_off, dst_cap, frame_len, ret);
+    return small ? launch_one<true, true>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
+                                          frame_len, ret)
+                 : launch_one<true, false>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
+                                           frame_len, ret);
   }
-  return hipGetLastError();
+  return small ? launch_one<false, true>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
+                                         frame_len, ret)
+               : launch_one<false, false>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
+                                          frame_len, ret);
 }
 
 }  // namespace kdb_lz4

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   const uint32_t head = stage_to_lds(g, (uint32_t)csize, s_in);
   __syncthreads();
   const int r = decode_block(s_in + head, csize, s_out, osize, tgt);
-  if (r > 0) flush_from_lds(o, s_out, 0, (uint32_t)r);
+  if (r > 0) flush_lds_to_global(o, s_out, 0, (uint32_t)r);
   if (lane == 0) {
     if (kFrame) {
       ret[v] = r > 0 ? 0 : -1;           // compressor.cc:109-115

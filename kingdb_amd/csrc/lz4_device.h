@@ -66,36 +66,42 @@ __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t b) {
 // Copies n bytes at global g (any alignment) into the 16B-aligned LDS buffer
 // `lds` with whole aligned 16-byte loads; byte i of the value lands at
 // lds[head + i] with head = g & 15 (returned).  An aligned 16-byte chunk never
-// crosses a page, so the over-read around [g, g+n) cannot fault.
+// crosses a page, so the over-read around [g, g+n) cannot fault.  The pointer
+// is rebased with pointer arithmetic (not via an integer) so the compiler keeps
+// the global address space: global_load_dwordx4, not flat.
 __device__ __forceinline__ uint32_t stage_to_lds(const uint8_t* g, uint32_t n, uint8_t* lds) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(g);
-  const uint32_t head = (uint32_t)(a & 15u);
-  const uint4* base = reinterpret_cast<const uint4*>(a - head);
+  const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+  const uint4* base = reinterpret_cast<const uint4*>(g - head);
   const uint32_t chunks = (head + n + 15u) >> 4;
   uint4* l = reinterpret_cast<uint4*>(lds);
   for (uint32_t c = lane_id(); c < chunks; c += 64u) l[c] = base[c];
   return head;
 }
 
-// Stores n bytes from LDS (value byte i at lds[head + i]) to global g (any
-// alignment): byte stores for the unaligned head/tail, dword stores between.
-__device__ __forceinline__ void flush_from_lds(uint8_t* g, const uint8_t* lds, uint32_t head,
-                                               uint32_t n) {
+// Stores bytes lds_base[off .. off+n) (lds_base 16B-aligned LDS) to global g
+// (any alignment): byte stores up to g's 16-byte boundary, then 16-byte stores
+// (ds_read_b128 when the LDS side is aligned too), then the tail.
+__device__ __forceinline__ void flush_lds_to_global(uint8_t* g, const uint8_t* lds_base, uint32_t off,
+                                                    uint32_t n) {
   const uint32_t lane = lane_id();
-  const uint32_t mis = (uint32_t)((4u - (reinterpret_cast<uintptr_t>(g) & 3u)) & 3u);
+  const uint32_t mis = (uint32_t)((16u - (reinterpret_cast<uintptr_t>(g) & 15u)) & 15u);
   const uint32_t pre = mis < n ? mis : n;
-  if (lane < pre) g[lane] = lds[head + lane];
-  const uint32_t body = (n - pre) >> 2;
-  uint32_t* gw = reinterpret_cast<uint32_t*>(g + pre);
-  const uint32_t sb = head + pre;
-  if ((sb & 3u) == 0) {
-    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds + sb);
-    for (uint32_t i = lane; i < body; i += 64u) gw[i] = lw[i];
+  if (lane < pre) g[lane] = lds_base[off + lane];
+  const uint32_t body = (n - pre) >> 4;
+  uint4* g4 = reinterpret_cast<uint4*>(g + pre);
+  const uint32_t sb = off + pre;
+  if ((sb & 15u) == 0) {
+    const uint4* l4 = reinterpret_cast<const uint4*>(lds_base + sb);
+    for (uint32_t i = lane; i < body; i += 64u) g4[i] = l4[i];
   } else {
-    for (uint32_t i = lane; i < body; i += 64u) gw[i] = lds_rd32(lds, sb + 4u * i);
+    for (uint32_t i = lane; i < body; i += 64u) {
+      const uint32_t b = sb + 16u * i;
+      g4[i] = make_uint4(lds_rd32(lds_base, b), lds_rd32(lds_base, b + 4u), lds_rd32(lds_base, b + 8u),
+                         lds_rd32(lds_base, b + 12u));
+    }
   }
-  const uint32_t done = pre + 4u * body;
-  if (lane < n - done) g[done + lane] = lds[head + done + lane];
+  const uint32_t done = pre + 16u * body;
+  if (lane < n - done) g[done + lane] = lds_base[off + done + lane];
 }
 
 }  // namespace kdb_lz4

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Builds ablation variants of libkdb_lz4.so into kingdb_amd/build/var_<name>.so
+set -e
+cd "$(dirname "$0")/../kingdb_amd"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc"
+for v in "$@"; do
+  name=${v%%:*}; flags=${v#*:}; [ "$flags" = "$v" ] && flags=""
+  d=build/var_$name; mkdir -p $d
+  for f in csrc/*.hip; do $H $flags -c $f -o $d/$(basename $f .hip).o & done; wait
+  /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -Icsrc -I../include -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -x c++ -c csrc/compressor.cc -o $d/compressor.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/var_$name.so $d/*.o -Wl,-rpath,/opt/rocm/lib
+done
