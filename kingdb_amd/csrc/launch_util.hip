@@ -1,0 +1,76 @@
+// kingdb_amd/csrc/launch_util.hip -- launch plumbing shared by the kernels:
+// persistent-grid sizing and the per-launch work counters they dequeue from.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+#include <unordered_map>
+
+namespace kdb_lz4 {
+
+namespace {
+// Per-device pool of 16-byte counter slots.  A launch takes the next slot
+// round-robin and zeroes it on its own stream (stream-ordered, so a slot is
+// reused only after 4096 later launches -- far more than can be in flight).
+constexpr uint32_t kSlots = 4096;
+struct Pool {
+  uint8_t* base = nullptr;
+  std::atomic<uint32_t> next{0};
+};
+std::mutex g_mu;
+std::unordered_map<int, Pool*> g_pools;
+}  // namespace
+
+hipError_t work_counter(hipStream_t st, uint32_t** ctr) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  Pool* p;
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    Pool*& slot = g_pools[dev];
+    if (!slot) {
+      slot = new Pool();
+      e = hipMalloc(&slot->base, (size_t)kSlots * 16u);
+      if (e != hipSuccess) {
+        delete slot;
+        slot = nullptr;
+        return e;
+      }
+    }
+    p = slot;
+  }
+  uint8_t* c = p->base + (size_t)(p->next.fetch_add(1) % kSlots) * 16u;
+  e = hipMemsetAsync(c, 0, 16, st);
+  *ctr = reinterpret_cast<uint32_t*>(c);
+  return e;
+}
+
+// Workgroups of 64 threads resident at once for `kern` with `lds` bytes of
+// dynamic LDS, capped at n (the kernels dequeue values dynamically, so a
+// workgroup that is admitted late simply takes fewer values).
+uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  uint64_t slots = (uint64_t)per_cu * (uint64_t)cus;
+#ifdef KDB_ABL_GRID_MULT
+  slots *= KDB_ABL_GRID_MULT;   // diagnostic: oversubscribe the persistent grid
+#endif
+  return (uint32_t)(n < slots ? n : slots);
+}
+
+// Values per counter claim: ~1/8 of a workgroup's share, at most 16, so the
+// claim rate stays far below one counter's ceiling and the tail stays short.
+uint32_t claim_batch(uint32_t n, uint32_t grid) {
+  uint64_t b = grid ? (uint64_t)n / ((uint64_t)grid * 8u) : 1u;
+  if (b < 1) b = 1;
+  if (b > 16) b = 16;
+  return (uint32_t)b;
+}
+
+}  // namespace kdb_lz4

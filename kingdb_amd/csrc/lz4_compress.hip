@@ -5,8 +5,8 @@
 // (lz4.cc:431-641), fused with CompressorLZ4::Compress's frame epilogue
 // (algorithm/compressor.cc:26-59).  Output is byte-identical to the reference.
 //
-// Persistent launch: one wavefront (workgroup of 64) per resident slot walks
-// the batch with a grid stride.  LDS per workgroup: the byU16 hash table
+// Persistent launch: one wavefront (workgroup of 64) per resident slot takes
+// values from a device-scope work counter, one value ahead.  LDS per workgroup: the byU16 hash table
 // (8192 x u16), the staged value and the block being assembled (flushed to HBM
 // with 16-byte stores).  For launches whose values are all <= 4 KiB the table
 // carries a 4-bit generation tag beside each 12-bit position, so it is cleared
@@ -29,6 +29,8 @@
 //    together: the match length after catching up c bytes is c + the length
 //    measured from the original position, so neither waits for the other;
 //  * literal copies and length-byte runs.
+#include <cstdio>
+
 #include "lz4_device.h"
 
 namespace kdb_lz4 {
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t in_cap,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
-    int32_t* __restrict__ ret) {
+    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
@@ -297,7 +299,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   }
   // register prefetch (kSmall): the next value's 16-byte chunks, lane-strided
   uint4 pf[kPrefetch];
-  uint32_t v = blockIdx.x;
+  WorkQueue wq{work, n, batch, 0u, 0u};
+  uint32_t v = wq.next();
   auto prefetch = [&](uint32_t w) {
     if (w < n) {
       const uint8_t* gp = src + src_off[w];
@@ -313,13 +316,15 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   };
   if (kSmall) prefetch(v);
 
-  for (; v < n; v += gridDim.x) {
+  while (v < n) {
+    const uint32_t vn = wq.next();         // the next value, one ahead
     const uint32_t S = uni(src_len[v]);
     const uint8_t* g = src + src_off[v];
     uint8_t* o = dst + dst_off[v];
     if (S > in_cap || S >= k64KLimit) {             // byU32 sizes: not this kernel
       if (lane == 0) { ret[v] = kUnsupported; if (kFrame) frame_len[v] = 0; }
-      if (kSmall) prefetch(v + gridDim.x);
+      if (kSmall) prefetch(vn);
+      v = vn;
       continue;
     }
     uint32_t head;
@@ -327,7 +332,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
 #pragma unroll
       for (uint32_t i = 0; i < kPrefetch; ++i) reinterpret_cast<uint4*>(s_in)[lane + 64u * i] = pf[i];
-      prefetch(v + gridDim.x);       // the next value's loads fly while this one is parsed
+      prefetch(vn);                  // the next value's loads fly while this one is parsed
     } else {
       head = stage_to_lds(g, S, s_in);
 #ifndef KDB_ABL_NO_ZERO
@@ -376,6 +381,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       }
     }
     __syncthreads();
+    v = vn;
   }
 }
 
@@ -394,16 +400,13 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret) {
   auto kern = lz4_compress_kernel<F, Sm>;
-  int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) != hipSuccess || per_cu < 1)
-    per_cu = 1;
-  (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-    cus = 256;
-  const uint64_t slots = (uint64_t)per_cu * (uint64_t)cus;
-  const uint32_t grid = (uint32_t)(n < slots ? n : slots);
+  uint32_t* work = nullptr;
+  hipError_t e = work_counter(st, &work);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, in_cap, dst, dst_off,
-                     dst_cap, frame_len, ret);
+                     dst_cap, frame_len, ret, work, batch);
   return hipGetLastError();
 }
 

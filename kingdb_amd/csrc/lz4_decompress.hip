@@ -1,96 +1,148 @@
 // kingdb_amd/csrc/lz4_decompress.hip -- gfx950 LZ4 r1.3.0 block decoder.
 //
 // Replaces LZ4_decompress_safe_partial (/root/reference/algorithm/lz4.cc:1050-1053)
-// = LZ4_decompress_generic(endOnInputSize, partial, target=max, noDict)
+// = LZ4_decompress_generic(endOnInputSize, partial, target, noDict)
 // (lz4.cc:876-1042), and -- in frame mode -- CompressorLZ4::Uncompress's frame
 // handling (algorithm/compressor.cc:75-137).  Successful decodes are bit-exact;
 // malformed blocks return the reference's exact code -(consumed)-1.
 //
-// One wavefront per value.  The compressed block is staged HBM -> LDS with
-// aligned 16-byte loads; the value is rebuilt in an LDS window (the match
-// source is always earlier output) and written back to HBM in one coalesced
-// pass.  Token/length parsing is wave-uniform scalar work; literal runs and
-// match copies are lane-parallel.  An overlapping match (offset < length) is a
-// periodic extension of the `offset` bytes before it, so lane i reads
-// out[ref + (i mod offset)] -- every source byte is already final and the copy
-// is one parallel pass (equivalent to the reference's dec32/dec64 trick,
-// lz4.cc:1008-1018).
+// Persistent launch; one wavefront per value at a time, values taken from a
+// device-scope work counter.  The compressed block
+// is staged HBM -> LDS with aligned 16-byte loads; the value is rebuilt in an
+// LDS window (a match source is always earlier output) and written back with
+// 16-byte stores.
+//
+// The decoder is instruction-issue bound, so its token stream is read from a
+// 256-byte register window (one dword per lane, refilled by one ds_read_b32):
+// four consecutive block bytes are two v_readlane + one 64-bit shift, with no
+// LDS round trip per token/offset/length byte.  Literal runs and match copies
+// are lane-parallel; an overlapping match (offset < length) is a periodic
+// extension of the `offset` bytes before it, so lane i reads
+// out[ref + (i mod offset)] -- every source byte is already final and one pass
+// suffices (the same bytes as the reference's dec32/dec64 copy, lz4.cc:1008-1018).
+#include <cstdio>
+
 #include "lz4_device.h"
 
 namespace kdb_lz4 {
 
-// Decodes the block at in[0..csize) into out[0..osize) (both LDS).
-// Bytes read at or past csize read as 0 (see oracle/lz4_oracle.c).
-__device__ int decode_block(const uint8_t* __restrict__ in, int csize, uint8_t* __restrict__ out,
-                            int osize, int target) {
+// 256-byte window over the staged block (LDS byte coordinates).
+struct Window {
+  const uint32_t* w32;   // LDS buffer as dwords
+  uint32_t base;         // LDS byte offset of lane 0's dword (multiple of 4)
+  uint32_t win;          // this lane's dword
+  __device__ __forceinline__ void load(uint32_t p) {   // window covering p..p+251
+    base = uni(p & ~3u);
+    win = w32[(base >> 2) + lane_id()];
+  }
+  // four bytes at LDS byte offset p (little endian)
+  __device__ __forceinline__ uint32_t get4(uint32_t p) {
+    if (p + 8u > base + 256u) load(p);
+    const uint32_t i = (p - base) >> 2;
+    const uint64_t q = ((uint64_t)readlane(win, i + 1u) << 32) | readlane(win, i);
+    return uni((uint32_t)(q >> (8u * (p & 3u))));
+  }
+};
+
+// Decodes the block at LDS bytes [in_off, in_off + csize) of `lds_in` into
+// out[0..osize) (LDS).  The 16 bytes after the block are zero (bytes read at or
+// past csize read as 0, see oracle/lz4_oracle.c).
+__device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off, int csize,
+                            uint8_t* __restrict__ out, int osize, int target) {
   const uint32_t lane = lane_id();
-  const int iend = csize, oend = osize;
-  const int oexit = min(target, oend - (int)kMfLimit);           // lz4.cc:908-910
-#define INB(i) ((uint32_t)uni(((i) >= 0 && (i) < iend) ? (uint32_t)in[(i)] : 0u))
-  if (osize == 0) return (csize == 1 && INB(0) == 0) ? 0 : -1;   // lz4.cc:911
+  in_off = uni(in_off);
+  const int iend = unii(csize), oend = unii(osize);
+  const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
+  const uint8_t* in = lds_in + in_off;
+  Window wd{reinterpret_cast<const uint32_t*>(lds_in), 0u, 0u};
+  wd.load(in_off);
+  if (osize == 0) return (csize == 1 && (wd.get4(in_off) & 0xffu) == 0) ? 0 : -1;   // lz4.cc:911
+  const float lanef = (float)lane;
   int ip = 0, op = 0;
+#pragma unroll 1
   for (;;) {
-    const uint32_t token = INB(ip);
+    ip = unii(ip);
+    op = unii(op);
+    uint32_t q = wd.get4(in_off + (uint32_t)ip);
+    const uint32_t token = q & 0xffu;
     ip++;
     int length = (int)(token >> 4);
     if (length == (int)kRunMask) {                                // lz4.cc:917-925
-      uint32_t s;
-      do {
-        s = INB(ip);
+      uint32_t s = (q >> 8) & 0xffu;
+      ip++;
+      length += (int)s;
+#pragma unroll 1
+      while (ip < iend - (int)kRunMask && s == 255u) {
+        s = wd.get4(in_off + (uint32_t)ip) & 0xffu;
         ip++;
         length += (int)s;
-      } while (ip < iend - (int)kRunMask && s == 255u);
+      }
     }
     const int cpy = op + length;                                  // lz4.cc:930-952
     const bool last = cpy > oexit || ip + length > iend - (int)(2 + 1 + kLastLiterals);
-    if (last) {
-      if (cpy > oend) return -ip - 1;
-      if (ip + length > iend) return -ip - 1;
+    if (last && (cpy > oend || ip + length > iend)) return -ip - 1;
+#pragma unroll 1
+    for (int i = 0; i < length; i += 64) {
+      const int j = i + (int)lane;
+      const uint8_t b = in[ip + j];
+      if (j < length) out[op + j] = b;
     }
-    for (int i = (int)lane; i < length; i += 64) out[op + i] = in[ip + i];
     ip += length;
     op = cpy;
     if (last) break;
-    // offset (lz4.cc:955-956)
-    const int off = (int)(INB(ip) | (INB(ip + 1) << 8));
+    // offset (lz4.cc:955-956) and the first match-length byte
+    q = wd.get4(in_off + (uint32_t)ip);
+    const int off = (int)(q & 0xffffu);
     ip += 2;
     const int ref = op - off;
     if (ref < 0) return -ip - 1;
-    // match length (lz4.cc:959-968)
-    length = (int)(token & kMlMask);
+    length = (int)(token & kMlMask);                              // lz4.cc:959-968
     if (length == (int)kMlMask) {
-      uint32_t s;
-      do {
+      if (ip > iend - (int)kLastLiterals) return -ip - 1;
+      uint32_t s = (q >> 16) & 0xffu;
+      ip++;
+      length += (int)s;
+#pragma unroll 1
+      while (s == 255u) {
         if (ip > iend - (int)kLastLiterals) return -ip - 1;
-        s = INB(ip);
+        s = wd.get4(in_off + (uint32_t)ip) & 0xffu;
         ip++;
         length += (int)s;
-      } while (s == 255u);
+      }
     }
     const int mlen = length + (int)kMinMatch;
-    if (op + mlen > oend - (int)kLastLiterals) return -ip - 1;   // lz4.cc:1024
+    if (op + mlen > oend - (int)kLastLiterals) return -ip - 1;    // lz4.cc:1024
     asm volatile("" ::: "memory");
-    if (off >= mlen) {
-      for (int i = (int)lane; i < mlen; i += 64) out[op + i] = out[ref + i];
+    if (off >= mlen || off >= 64) {
+      // plain forward copy in 64-byte steps: every source byte is < the step
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) {
+        const int j = i + (int)lane;
+        const uint8_t b = out[ref + j];
+        if (j < mlen) out[op + j] = b;
+        asm volatile("" ::: "memory");
+      }
     } else if (off > 0) {
-      // periodic: out[op+i] = out[ref + i mod off]
-      int j = (int)lane % off;
-      const int step = 64 % off;
-      for (int i = (int)lane; i < mlen; i += 64) {
-        out[op + i] = out[ref + j];
-        j += step;
-        if (j >= off) j -= off;
+      // periodic: out[op+j] = out[ref + j mod off]   (j mod off via f32 reciprocal)
+      const float rcp = __builtin_amdgcn_rcpf((float)off);
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) {
+        const int j = i + (int)lane;
+        const int qd = (int)(((float)i + lanef) * rcp);
+        int r = j - qd * off;
+        if (r >= off) r -= off;
+        const uint8_t b = out[ref + r];
+        if (j < mlen) out[op + j] = b;
       }
     }  // off == 0: the reference copies the destination onto itself
     asm volatile("" ::: "memory");
     op += mlen;
   }
-#undef INB
   return op;
 }
 
-// kFrame = false: block mode. in_len[v] = C, out_cap[v] = S (target = max);
-//   ret[v] = LZ4 return code, out_len[v] = max(ret, 0).
+// kFrame = false: block mode. in_len[v] = C, out_cap[v] = S (target = max unless
+//   given); ret[v] = LZ4 return code, out_len[v] = max(ret, 0).
 // kFrame = true : one CompressorLZ4 frame per value at src + src_off[v]
 //   (header u32 size_compressed_stored, u32 size_source); in_len[v] = bytes
 //   available there; ret[v] = 0 (OK) / -1 (IOError); out_len[v] = *size_dest.
@@ -100,73 +152,95 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret) {
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t v = blockIdx.x;
-  if (v >= n) return;
   const uint32_t lane = lane_id();
-  const uint8_t* g = src + src_off[v];
-  uint8_t* o = dst + dst_off[v];
-  int csize, osize, tgt;
-  if (kFrame) {
-    // compressor.cc:89-90 (GetFixed32 x2)
-    const uint32_t stored =
-        uni((uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[2] << 16) | ((uint32_t)g[3] << 24));
-    const uint32_t raw =
-        uni((uint32_t)g[4] | ((uint32_t)g[5] << 8) | ((uint32_t)g[6] << 16) | ((uint32_t)g[7] << 24));
-    const uint32_t avail = uni(in_len[v]);
-    if (raw > out_cap[v]) {
-      if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
-      return;
-    }
-    if (stored == 0) {  // raw frame (compressor.cc:116-124)
-      if (raw + 8u > avail) {
-        if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
-        return;
-      }
-      for (uint32_t i = lane; i < raw; i += 64u) o[i] = g[8u + i];
-      if (lane == 0) { ret[v] = 0; out_len[v] = raw; }
-      return;
-    }
-    csize = (int)(stored - 8u);          // compressor.cc:96 (u32 wrap kept: int cast)
-    osize = (int)raw;
-    tgt = osize;                         // compressor.cc:103-107: target = max = size_source
-    g += 8;
-    if (csize < 0 || (uint32_t)csize + 8u > avail) {
-      // a negative size makes the reference return -2/-3 (IOError); a size past
-      // the bytes supplied would have it read foreign memory: IOError as well.
-      if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
-      return;
-    }
-  } else {
-    csize = (int)uni(in_len[v]);
-    osize = (int)uni(out_cap[v]);
-    tgt = target ? (int)uni(target[v]) : osize;
-  }
-  if ((uint32_t)csize > in_cap || (uint32_t)osize > out_cap_max || csize < 0 || osize < 0) {
-    if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
-    return;
-  }
-  const uint32_t out_bytes = (out_cap_max + 15u) & ~15u;
+  const uint32_t out_bytes = ((out_cap_max + 15u) & ~15u) + 16u;
   uint8_t* s_out = smem;
-  uint8_t* s_in = smem + out_bytes + 16u;
-  const uint32_t head = stage_to_lds(g, (uint32_t)csize, s_in);
-  __syncthreads();
-  const int r = decode_block(s_in + head, csize, s_out, osize, tgt);
-  if (r > 0) flush_lds_to_global(o, s_out, 0, (uint32_t)r);
-  if (lane == 0) {
+  uint8_t* s_in = smem + out_bytes;
+
+  WorkQueue wq{work, n, batch, 0u, 0u};
+#pragma unroll 1
+  for (uint32_t v = wq.next(); v < n; v = wq.next()) {
+    const uint8_t* g = src + src_off[v];
+    uint8_t* o = dst + dst_off[v];
+    int csize, osize, tgt;
     if (kFrame) {
-      ret[v] = r > 0 ? 0 : -1;           // compressor.cc:109-115
-      out_len[v] = r > 0 ? (uint32_t)r : 0u;
+      // compressor.cc:89-90 (GetFixed32 x2)
+      const uint32_t stored =
+          uni((uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[2] << 16) | ((uint32_t)g[3] << 24));
+      const uint32_t raw =
+          uni((uint32_t)g[4] | ((uint32_t)g[5] << 8) | ((uint32_t)g[6] << 16) | ((uint32_t)g[7] << 24));
+      const uint32_t avail = uni(in_len[v]);
+      if (raw > uni(out_cap[v])) {
+        if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+        continue;
+      }
+      if (stored == 0) {  // raw frame (compressor.cc:116-124)
+        if (raw + 8u > avail) {
+          if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+          continue;
+        }
+        for (uint32_t i = lane; i < raw; i += 64u) o[i] = g[8u + i];
+        if (lane == 0) { ret[v] = 0; out_len[v] = raw; }
+        continue;
+      }
+      csize = (int)(stored - 8u);          // compressor.cc:96 (u32 wrap kept: int cast)
+      osize = (int)raw;
+      tgt = osize;                         // compressor.cc:103-107: target = max = size_source
+      g += 8;
+      if (csize < 0 || (uint32_t)csize + 8u > avail) {
+        // a negative size makes the reference return -2/-3 (IOError); a size past
+        // the bytes supplied would have it read foreign memory: IOError as well.
+        if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+        continue;
+      }
     } else {
-      ret[v] = r;
-      if (out_len) out_len[v] = r > 0 ? (uint32_t)r : 0u;
+      csize = (int)uni(in_len[v]);
+      osize = (int)uni(out_cap[v]);
+      tgt = target ? (int)uni(target[v]) : osize;
     }
+    if ((uint32_t)csize > in_cap || (uint32_t)osize > out_cap_max || csize < 0 || osize < 0) {
+      if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
+      continue;
+    }
+    const uint32_t head = stage_to_lds(g, (uint32_t)csize, s_in);
+    if (lane < 16u) s_in[head + (uint32_t)csize + lane] = 0;   // OOB bytes read as 0
+    __syncthreads();
+    const int r = decode_block(s_in, head, csize, s_out, osize, tgt);
+    if (r > 0) flush_lds_to_global(o, s_out, 0, (uint32_t)r);
+    if (lane == 0) {
+      if (kFrame) {
+        ret[v] = r > 0 ? 0 : -1;           // compressor.cc:109-115
+        out_len[v] = r > 0 ? (uint32_t)r : 0u;
+      } else {
+        ret[v] = r;
+        if (out_len) out_len[v] = r > 0 ? (uint32_t)r : 0u;
+      }
+    }
+    __syncthreads();
   }
 }
 
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
-  return (((size_t)max_out + 15u) & ~(size_t)15u) + 16u + (((size_t)max_in + 15u) & ~(size_t)15u) + 48u;
+  // out window | staged block + zero tail + the register window's 256-byte reach
+  return (((size_t)max_out + 15u) & ~(size_t)15u) + 16u + (((size_t)max_in + 15u) & ~(size_t)15u) + 320u;
+}
+
+template <bool F>
+static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
+                             const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out, uint8_t* dst,
+                             const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
+                             uint32_t* out_len, int32_t* ret) {
+  auto kern = lz4_decompress_kernel<F>;
+  uint32_t* work = nullptr;
+  hipError_t e = work_counter(st, &work);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  const uint32_t batch = claim_batch(n, grid);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
+                     out_cap, target, out_len, ret, work, batch);
+  return hipGetLastError();
 }
 
 hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
@@ -175,14 +249,10 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   if (n == 0) return hipSuccess;
   const size_t lds = decompress_lds_bytes(max_in, max_out);
-  if (frame) {
-    hipLaunchKernelGGL(lz4_decompress_kernel<true>, dim3(n), dim3(64), lds, st, src, src_off, in_len,
-                       n, max_in, max_out, dst, dst_off, out_cap, target, out_len, ret);
-  } else {
-    hipLaunchKernelGGL(lz4_decompress_kernel<false>, dim3(n), dim3(64), lds, st, src, src_off,
-                       in_len, n, max_in, max_out, dst, dst_off, out_cap, target, out_len, ret);
-  }
-  return hipGetLastError();
+  return frame ? launch_one<true>(st, lds, src, src_off, in_len, n, max_in, max_out, dst, dst_off, out_cap,
+                                  target, out_len, ret)
+               : launch_one<false>(st, lds, src, src_off, in_len, n, max_in, max_out, dst, dst_off, out_cap,
+                                   target, out_len, ret);
 }
 
 }  // namespace kdb_lz4

@@ -50,6 +50,29 @@ __device__ __forceinline__ uint32_t first_zero(uint64_t m) {
   return z ? (uint32_t)__builtin_ctzll(z) : 64u;
 }
 
+// Dynamic work distribution of the persistent kernels.  Lane 0 claims `batch`
+// consecutive value indices with one device-scope atomic; a single counter
+// saturates near 88 claims/us (microarch "dequeue"), so claims are batched to
+// stay far below that.  next() hands out values one ahead of their use.
+struct WorkQueue {
+  uint32_t* ctr;
+  uint32_t n, batch, cur, end;
+  __device__ __forceinline__ void claim() {
+    uint32_t v = 0;
+    if (lane_id() == 0) v = atomicAdd(ctr, batch);
+    cur = uni(v);
+    end = min(cur + batch, n);
+  }
+  __device__ __forceinline__ uint32_t next() {   // n when the batch is exhausted
+    if (cur >= end) {
+      if (end >= n && cur >= n) return n;
+      claim();
+      if (cur >= n) return n;
+    }
+    return cur++;
+  }
+};
+
 // LZ4_compressBound (lz4.h:103).
 __host__ __device__ __forceinline__ uint32_t compress_bound(uint32_t n) {
   return n > kMaxInput ? 0u : n + n / 255u + 16u;
@@ -103,5 +126,9 @@ __device__ __forceinline__ void flush_lds_to_global(uint8_t* g, const uint8_t* l
   const uint32_t done = pre + 16u * body;
   if (lane < n - done) g[done + lane] = lds_base[off + done + lane];
 }
+
+hipError_t work_counter(hipStream_t st, uint32_t** ctr);
+uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
+uint32_t claim_batch(uint32_t n, uint32_t grid);
 
 }  // namespace kdb_lz4

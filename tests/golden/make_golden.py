@@ -132,6 +132,7 @@ def main() -> None:
         tgt = size if rng.random() < 0.8 else rng.randrange(-2, size + 30)
         r, out = ref_decode(ref, blk, size, tgt)
         ro, oo = orc_decode(orc, blk, size, tgt)
+        _, oo_ff = orc_decode(orc, blk, size, tgt, fill=0xFF)
         assert ro == r, (blk.hex(), size, tgt, ro, r)
         m_blk.append(blk)
         m_size.append(size)
@@ -139,8 +140,10 @@ def main() -> None:
         m_ret.append(r)
         m_out.append(out)
         # output bytes are specified unless the block used offset 0 (the
-        # reference then copies uninitialised destination bytes).
-        m_cmp.append(1 if (r <= 0 or oo == out) else 0)
+        # reference then copies destination bytes it never wrote, so the
+        # result depends on the buffer's prior contents): detected by decoding
+        # into a 0x00- and a 0xFF-filled buffer.
+        m_cmp.append(1 if (r <= 0 or (oo == out and oo == oo_ff)) else 0)
     b_d, b_o, b_l = cat(m_blk)
     o_d, o_o, o_l = cat(m_out)
     np.savez_compressed(os.path.join(OUT, "malformed.npz"), blk=b_d, blk_off=b_o, blk_len=b_l,
@@ -197,10 +200,10 @@ def ref_decode(ref: oracle.Reference, blk: bytes, size: int, tgt: int):
     return r, (dst[:r].tobytes() if r > 0 else b"")
 
 
-def orc_decode(orc: oracle.Oracle, blk: bytes, size: int, tgt: int):
+def orc_decode(orc: oracle.Oracle, blk: bytes, size: int, tgt: int, fill: int = 0):
     src = np.zeros(len(blk) + 64, np.uint8)
     src[: len(blk)] = np.frombuffer(blk, np.uint8)
-    dst = np.zeros(max(size, 0) + 64, np.uint8)
+    dst = np.full(max(size, 0) + 64, fill, np.uint8)
     r = orc.lib.orc_decompress_safe_partial(oracle._ptr(src), oracle._ptr(dst), len(blk), tgt, size)
     return r, (dst[:r].tobytes() if r > 0 else b"")
 
