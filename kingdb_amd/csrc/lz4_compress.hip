@@ -6,13 +6,16 @@
 // (algorithm/compressor.cc:26-59).  Output is byte-identical to the reference.
 //
 // Persistent launch: one wavefront (workgroup of 64) per resident slot takes
-// values from a device-scope work counter, one value ahead.  LDS per workgroup: the byU16 hash table
-// (8192 x u16), the staged value and the block being assembled (flushed to HBM
-// with 16-byte stores).  For launches whose values are all <= 4 KiB the table
-// carries a 4-bit generation tag beside each 12-bit position, so it is cleared
-// once per 15 values instead of per value (a stale tag reads as the zeroed
-// slot, position 0 -- lz4.cc:669 semantics), and the next value is prefetched
-// into registers while the current one is parsed.
+// values from a device-scope work counter, one value ahead.  LDS per
+// workgroup = the byU16 hash table (8192 x u16) + the value, realigned to
+// offset 0 while it is staged: 20 KiB for 4 KiB values, i.e. 8 resident
+// values per CU.  Every LDS read is clamped into that region.  For launches
+// whose values are all <= 4 KiB the table carries a 4-bit generation tag beside
+// each 12-bit position, so it is cleared once per 15 values instead of per
+// value (a stale tag reads as the zeroed slot, position 0 -- lz4.cc:669
+// semantics), and the next value is prefetched into registers while the
+// current one is parsed.  Each sequence's bytes (token, length runs, literals,
+// offset) are written straight to HBM by one wave-wide store per 64 bytes.
 //
 // The greedy parse is sequential by definition; what is parallel is:
 //  * the search loop (lz4.cc:494-527): the positions it visits from a start
@@ -28,9 +31,7 @@
 //  * the catch-up loop (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued
 //    together: the match length after catching up c bytes is c + the length
 //    measured from the original position, so neither waits for the other;
-//  * literal copies and length-byte runs.
-#include <cstdio>
-
+//  * the byte emission of a sequence.
 #include "lz4_device.h"
 
 namespace kdb_lz4 {
@@ -46,6 +47,8 @@ __device__ __forceinline__ uint32_t search_pos(uint32_t s, uint32_t k) {
 __device__ __forceinline__ uint32_t search_step(uint32_t k) { return k == 0 ? 1u : (63u + k) >> 6; }
 
 __device__ __forceinline__ uint32_t hash16(uint32_t seq) { return (seq * 2654435761u) >> 19; }
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // The byU16 table.  kTagged: entry = gen << 12 | pos (values <= 4 KiB, so
 // positions < 4096); an entry of another generation is an empty slot (0).
@@ -63,61 +66,61 @@ struct Table {
   }
 };
 
-// Output: the block is assembled in LDS (out[0..out_cap)) and flushed to HBM
-// once complete.  kGuard (LZ4_compress_limitedOutput with a caller cap below
-// the bound): never write at or past out_cap -- the reference may, on
-// limitedOutput failures; the return value is what parity is about (see
-// oracle/lz4_oracle.c).  Without kGuard the cap is the bound, which the block
-// never exceeds.
+// Output: bytes go straight to HBM at out[0..).  kGuard (LZ4_compress_limitedOutput
+// with a caller cap below the bound): never write at or past out_cap -- the
+// reference may, on limitedOutput failures; the return value is what parity is
+// about (see oracle/lz4_oracle.c).  Without kGuard the slot holds the bound,
+// which the block never exceeds.
+//
+// Writes the encoding of one sequence at out[pos .. pos+total): token, the
+// literal-length run (nl bytes of 255 + remL, present iff lit >= 15), the
+// literals in[anchor .. anchor+lit), and -- when has_match -- the offset (LE16)
+// and the match-length run (nm bytes of 255 + remM, present iff long_ml).
+// One global_store_byte per 64 bytes.  Returns total.
 template <bool kGuard>
-__device__ __forceinline__ void put8(uint8_t* out, int out_cap, int pos, uint32_t b) {
-  if (!kGuard || (uint32_t)pos < (uint32_t)out_cap) out[pos] = (uint8_t)b;
-}
-
-// Lanes 0..nb write a length continuation (nb 255s then `rem`) at out[pos..].
-template <bool kGuard>
-__device__ __forceinline__ void put_len(uint8_t* out, int out_cap, int pos, uint32_t nb, uint32_t rem) {
+__device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, int pos, uint32_t token,
+                                        uint32_t lit, uint32_t nl, uint32_t remL, const uint8_t* in,
+                                        uint32_t S, uint32_t anchor, bool has_match, uint32_t off,
+                                        bool long_ml, uint32_t nm, uint32_t remM) {
   const uint32_t lane = lane_id();
+  const uint32_t a = 1u + (lit >= kRunMask ? nl + 1u : 0u);      // first literal byte
+  const uint32_t b = a + lit;                                      // offset low byte
+  const uint32_t total = has_match ? b + 2u + (long_ml ? nm + 1u : 0u) : b;
+#ifndef KDB_ABL_NO_EMIT
 #pragma unroll 1
-  for (uint32_t i = 0; i <= nb; i += 64u) {
+  for (uint32_t i = 0; i < total; i += 64u) {
     const uint32_t j = i + lane;
-    if (j <= nb) put8<kGuard>(out, out_cap, pos + (int)j, j < nb ? 255u : rem);
+    const uint32_t li = min(anchor + (j - a), S - 1u);             // clamped LDS read
+    const uint32_t lb = in[(j >= a && j < b) ? li : 0u];
+    uint32_t val;
+    if (j == 0) val = token;
+    else if (j < a) val = (j - 1u < nl) ? 255u : remL;
+    else if (j < b) val = lb;
+    else if (j == b) val = off & 255u;
+    else if (j == b + 1u) val = off >> 8;
+    else val = (j - b - 2u < nm) ? 255u : remM;
+    if (j < total && (!kGuard || pos + (int)j < out_cap)) out[pos + (int)j] = (uint8_t)val;
   }
-}
-
-// out[pos .. pos+n) = in[a .. a+n), 64 bytes per step.
-template <bool kGuard>
-__device__ __forceinline__ void put_bytes(uint8_t* out, int out_cap, int pos, const uint8_t* in, uint32_t a,
-                                          uint32_t n) {
-#ifdef KDB_ABL_NO_EMIT
-  return;
 #endif
-  const uint32_t lane = lane_id();
-#pragma unroll 1
-  for (uint32_t i = 0; i < n; i += 64u) {
-    const uint32_t j = i + lane;
-    const uint32_t b = in[a + j];
-    if (j < n) put8<kGuard>(out, out_cap, pos + (int)j, b);
-  }
+  return (int)total;
 }
 
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
-// in[i]; in_base/head: the 16B-aligned buffer and the offset of byte 0; the
-// buffer is readable well past S, so reads are issued unconditionally and
-// masked afterwards.  Returns the block size or 0 (limitedOutput failure,
-// checked against `cap` at the reference's check points), like the reference.
+// in[i], i < S (every read is clamped into [0, S)).  Returns the block size
+// or 0 (limitedOutput failure, checked against `cap` at the reference's check
+// points), like the reference.
 template <bool kTagged, bool kGuard>
-__device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_base, uint32_t head,
-                              uint32_t S, const Table<kTagged>& tab, uint8_t* __restrict__ out, int out_cap,
-                              int cap) {
+__device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const Table<kTagged>& tab,
+                              uint8_t* __restrict__ out, int out_cap, int cap) {
   const uint32_t lane = lane_id();
   int op = 0;
   uint32_t anchor = 0;
-#define RD32(p) lds_rd32(in_base, head + (p))
+#define RD32(p) lds_rd32(in, (p))
 
   if (S >= kMinLength) {                                    // lz4.cc:483
     const uint32_t mflimit = S - kMfLimit;
     const uint32_t matchlimit = S - kLastLiterals;
+    const uint32_t last4 = S - 4u;                          // highest position a u32 read may start
     // lz4.cc:486: put(0) stores position 0 -- what an empty slot already reads as.
     uint32_t s = 1;                                         // lz4.cc:487
     for (;;) {
@@ -129,24 +132,24 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
         const uint32_t k = kb + lane;
         const uint32_t pk = search_pos(s, k);
         const bool valid = pk + search_step(k) <= mflimit;         // lz4.cc:510
-        const uint32_t seq = RD32(pk);
+        const uint32_t seq = RD32(min(pk, last4));
         const uint32_t h = hash16(seq);
         const uint32_t told = tab.get(h);
-        const uint64_t vm = __ballot(valid);
+        const uint64_t vm = ballot(valid);
         // lanes of this chunk whose iteration hashes to the same slot
         uint32_t lo = ~0u, hi = ~0u;
 #pragma unroll
-        for (int b = 0; b < 13; ++b) {
-          const uint32_t t = (uint32_t)((int32_t)(h << (31 - b)) >> 31);   // 0 or ~0
-          const uint64_t m = __ballot(t != 0u);
+        for (int bb = 0; bb < 13; ++bb) {
+          const uint32_t t = (uint32_t)((int32_t)(h << (31 - bb)) >> 31);   // 0 or ~0
+          const uint64_t m = ballot(t != 0u);
           lo &= ~(t ^ (uint32_t)m);
           hi &= ~(t ^ (uint32_t)(m >> 32));
         }
         const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;
         const uint64_t below = same & mask_lt(lane);
         const uint32_t refk = below ? search_pos(s, kb + 63u - (uint32_t)__builtin_clzll(below)) : told;
-        const bool match = valid && RD32(refk) == seq;           // lz4.cc:527
-        const uint64_t mm = __ballot(match);
+        const bool match = valid && RD32(min(refk, last4)) == seq;   // lz4.cc:527
+        const uint64_t mm = ballot(match);
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
           const uint64_t later = same & ~mask_le(lane) & mask_le(ks);
@@ -169,15 +172,18 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
         {
           const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
           const uint32_t rem = matchlimit - (ip + kMinMatch);
-          const uint32_t a0 = in[ip - 1u - lane], b0 = in[ref - 1u - lane];
-          const uint32_t a1 = in[ip + kMinMatch + lane], b1 = in[ref + kMinMatch + lane];
-          c = first_zero(__ballot(lane < lim && a0 == b0));      // <= lim
-          ml = first_zero(__ballot(lane < rem && a1 == b1));     // <= rem
+          const bool cl = lane < lim, ml_in = lane < rem;
+          const uint32_t a0 = in[cl ? ip - 1u - lane : 0u], b0 = in[cl ? ref - 1u - lane : 0u];
+          const uint32_t a1 = in[ml_in ? ip + kMinMatch + lane : 0u];
+          const uint32_t b1 = in[ml_in ? ref + kMinMatch + lane : 0u];
+          c = first_zero(ballot(cl && a0 == b0));      // <= lim: lanes past it vote false
+          ml = first_zero(ballot(ml_in && a1 == b1));  // <= rem
           if (c == 64u) {
 #pragma unroll 1
             for (;;) {
-              const uint32_t x = in[ip - c - 1u - lane], y = in[ref - c - 1u - lane];
-              const uint32_t d = first_zero(__ballot(lane < lim - c && x == y));
+              const bool l2 = lane < lim - c;
+              const uint32_t x = in[l2 ? ip - c - 1u - lane : 0u], y = in[l2 ? ref - c - 1u - lane : 0u];
+              const uint32_t d = first_zero(ballot(l2 && x == y));
               c += d;
               if (d < 64u) break;
             }
@@ -185,8 +191,10 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
           if (ml == 64u) {
 #pragma unroll 1
             for (;;) {
-              const uint32_t x = in[ip + kMinMatch + ml + lane], y = in[ref + kMinMatch + ml + lane];
-              const uint32_t d = first_zero(__ballot(lane < rem - ml && x == y));
+              const bool l2 = lane < rem - ml;
+              const uint32_t x = in[l2 ? ip + kMinMatch + ml + lane : 0u];
+              const uint32_t y = in[l2 ? ref + kMinMatch + ml + lane : 0u];
+              const uint32_t d = first_zero(ballot(l2 && x == y));
               ml += d;
               if (d < 64u) break;
             }
@@ -199,30 +207,15 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
 
         // ======== token + literals (lz4.cc:535-550), offset (554), match length (580-592)
         const uint32_t lit = ip - anchor;
-        const int tok_pos = op;
-        op += 1;
-        if ((int64_t)op + lit + (2 + 1 + kLastLiterals) + lit / 255u > (int64_t)cap) return 0;
-        uint32_t token = (lit >= kRunMask ? kRunMask : lit) << 4;
-        if (lit >= kRunMask) {
-          const uint32_t nb = (lit - kRunMask) / 255u;
-          put_len<kGuard>(out, out_cap, op, nb, lit - kRunMask - 255u * nb);
-          op += (int)nb + 1;
-        }
-        put_bytes<kGuard>(out, out_cap, op, in, anchor, lit);
-        op += (int)lit;
-        const uint32_t off = ip - ref;
-        if (lane < 2u) put8<kGuard>(out, out_cap, op + (int)lane, lane ? (off >> 8) : (off & 255u));
-        op += 2;
-        if (ml >= kMlMask) {
-          if ((int64_t)op + (1 + kLastLiterals) + (ml >> 8) > (int64_t)cap) return 0;
-          token += kMlMask;
-          const uint32_t nb = (ml - kMlMask) / 255u;
-          put_len<kGuard>(out, out_cap, op, nb, ml - kMlMask - 255u * nb);
-          op += (int)nb + 1;
-        } else {
-          token += ml;
-        }
-        if (lane == 0) put8<kGuard>(out, out_cap, tok_pos, token);
+        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 0;
+        const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
+        const bool long_ml = ml >= kMlMask;
+        if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
+        const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
+        const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
+        const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
+        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
+                               true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
         ip = ip_end;
         anchor = ip;
         if (ip > mflimit) goto last_literals;                      // lz4.cc:597
@@ -248,30 +241,45 @@ __device__ int compress_block(const uint8_t* __restrict__ in, const uint8_t* in_
 last_literals:
   {  // lz4.cc:627-637
     const uint32_t run = S - anchor;
-    if ((int64_t)op + run + 1 + (run + 255u - kRunMask) / 255u > (int64_t)(uint32_t)cap) return 0;
-    if (lane == 0) put8<kGuard>(out, out_cap, op, (run >= kRunMask ? kRunMask : run) << 4);
-    op += 1;
-    if (run >= kRunMask) {
-      const uint32_t nb = (run - kRunMask) / 255u;
-      put_len<kGuard>(out, out_cap, op, nb, run - kRunMask - 255u * nb);
-      op += (int)nb + 1;
-    }
-    put_bytes<kGuard>(out, out_cap, op, in, anchor, run);
-    op += (int)run;
+    if (op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
+    const uint32_t nl = run >= kRunMask ? (run - kRunMask) / 255u : 0u;
+    op += emit_seq<kGuard>(out, out_cap, op, (run >= kRunMask ? kRunMask : run) << 4, run, nl,
+                           run - kRunMask - 255u * nl, in, S, anchor, false, 0u, false, 0u, 0u);
   }
 #undef RD32
   return op;
 }
 
 constexpr uint32_t kSmallMax = 4096u;     // tagged table + register prefetch
-constexpr uint32_t kPrefetch = 5u;        // 16-byte loads per lane: (15 + 4096 + 15) / 16 / 64 < 5
+constexpr uint32_t kPrefetch = 4u;        // output chunks per lane: 4096 / 16 / 64
 
-// Staged-input region: value bytes + 16-byte-load slack; the register prefetch
-// of small launches writes kPrefetch whole KiB.
-__host__ __device__ __forceinline__ uint32_t in_region_bytes(bool small, uint32_t in_cap) {
-  const uint32_t a = ((in_cap + 15u) & ~15u) + 48u;
-  const uint32_t b = small ? kPrefetch * 64u * 16u + 16u : 0u;
-  return a > b ? a : b;
+// out chunk = bytes [sh, sh+16) of the 32 bytes (a, b); sh in 0..15 (uniform)
+__device__ __forceinline__ uint4 funnel16(const uint4& a, const uint4& b, uint32_t sh) {
+  if (sh == 0) return a;
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const uint32_t q = sh >> 2, r = sh & 3u;
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t lo = w[k], hi = w[k + 1];
+    // select w[k+q], w[k+q+1] with a uniform q (0..3)
+    if (q == 1) { lo = w[k + 1]; hi = w[k + 2]; }
+    else if (q == 2) { lo = w[k + 2]; hi = w[k + 3]; }
+    else if (q == 3) { lo = w[k + 3]; hi = w[k + 4]; }
+    o[k] = __builtin_amdgcn_alignbyte(hi, lo, r);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Stages value bytes g[0 .. n) into LDS at offset 0 (16B-aligned), whatever
+// g's alignment: whole aligned 16-byte loads (an aligned chunk never crosses a
+// page, so the over-read cannot fault), realigned in registers.
+__device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint8_t* lds) {
+  const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+  const uint4* base = reinterpret_cast<const uint4*>(g - head);
+  const uint32_t chunks = (n + 15u) >> 4;
+  uint4* l = reinterpret_cast<uint4*>(lds);
+  for (uint32_t c = lane_id(); c < chunks; c += 64u) l[c] = head ? funnel16(base[c], base[c + 1u], head) : base[c];
 }
 
 // kFrame = false: LZ4_compress_limitedOutput per value; ret[v] = size or 0,
@@ -288,29 +296,29 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
-  uint8_t* s_in = smem + kTableBytes;
-  const uint32_t in_bytes = in_region_bytes(kSmall, in_cap);
-  uint8_t* s_out = s_in + in_bytes;       // [8-byte frame header][block]
+  uint8_t* s_in = smem + kTableBytes;    // value bytes [0, S), 16B-aligned
   const uint4 z4 = make_uint4(0, 0, 0, 0);
 
   Table<kSmall> tab{tab16, 1u};
   if (kSmall) {
     for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
   }
-  // register prefetch (kSmall): the next value's 16-byte chunks, lane-strided
-  uint4 pf[kPrefetch];
+  // register prefetch (kSmall): the next value's realigned 16-byte chunks
+  uint4 pa[kPrefetch], pb[kPrefetch];
+  uint32_t p_head = 0, p_chunks = 0;
   WorkQueue wq{work, n, batch, 0u, 0u};
   uint32_t v = wq.next();
   auto prefetch = [&](uint32_t w) {
     if (w < n) {
       const uint8_t* gp = src + src_off[w];
-      const uint32_t hd = (uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u);
-      const uint4* base = reinterpret_cast<const uint4*>(gp - hd);
-      const uint32_t chunks = (hd + min(src_len[w], kSmallMax) + 15u) >> 4;
+      p_head = uni((uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u));
+      const uint4* base = reinterpret_cast<const uint4*>(gp - p_head);
+      p_chunks = uni((min(src_len[w], kSmallMax) + 15u) >> 4);
 #pragma unroll
       for (uint32_t i = 0; i < kPrefetch; ++i) {
         const uint32_t c = lane + 64u * i;
-        pf[i] = c < chunks ? base[c] : z4;
+        pa[i] = c < p_chunks ? base[c] : z4;
+        pb[i] = (p_head && c < p_chunks) ? base[c + 1u] : z4;
       }
     }
   };
@@ -327,47 +335,39 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       v = vn;
       continue;
     }
-    uint32_t head;
     if (kSmall) {
-      head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
 #pragma unroll
-      for (uint32_t i = 0; i < kPrefetch; ++i) reinterpret_cast<uint4*>(s_in)[lane + 64u * i] = pf[i];
+      for (uint32_t i = 0; i < kPrefetch; ++i) {
+        const uint32_t c = lane + 64u * i;
+        if (c < p_chunks) reinterpret_cast<uint4*>(s_in)[c] = funnel16(pa[i], pb[i], p_head);
+      }
       prefetch(vn);                  // the next value's loads fly while this one is parsed
     } else {
-      head = stage_to_lds(g, S, s_in);
+      stage_aligned(g, S, s_in);
 #ifndef KDB_ABL_NO_ZERO
       for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
 #endif
     }
     __syncthreads();
 
-    const uint8_t* in = s_in + head;
     const uint32_t bound = compress_bound(S);
     if (!kFrame) {
       const uint32_t cap = uni(dst_cap[v]);
-      // the block never needs more than `bound` bytes; a larger cap changes nothing
-      const int r = cap < bound
-                        ? compress_block<kSmall, true>(in, s_in, head, S, tab, s_out + 8, (int)cap, (int)cap)
-                        : compress_block<kSmall, false>(in, s_in, head, S, tab, s_out + 8, (int)bound, (int)cap);
-      if (r > 0) flush_lds_to_global(o, s_out, 8, (uint32_t)r);
+      const int r = cap < bound ? compress_block<kSmall, true>(s_in, S, tab, o, (int)cap, (int)cap)
+                                : compress_block<kSmall, false>(s_in, S, tab, o, (int)bound, (int)cap);
       if (lane == 0) ret[v] = r;
     } else {
-      const int r = compress_block<kSmall, false>(in, s_in, head, S, tab, s_out + 8, (int)bound, (int)bound);
+      const int r = compress_block<kSmall, false>(s_in, S, tab, o + 8, (int)bound, (int)bound);
       if (r <= 0) {                              // compressor.cc:31-34
         if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
       } else {
         const bool raw = (uint32_t)r > S;        // raw fallback (compressor.cc:40-48)
         const uint32_t stored = raw ? 0u : (uint32_t)r + 8u;
         const uint32_t flen = raw ? S + 8u : stored;
+        if (raw) flush_lds_to_global(o + 8, s_in, 0, S);
         if (lane < 8u) {                         // compressor.cc:53-54
           const uint32_t w = lane < 4u ? stored : S;
-          s_out[lane] = (uint8_t)(w >> (8u * (lane & 3u)));
-        }
-        if (raw) {
-          flush_lds_to_global(o, s_out, 0, 8u);
-          flush_lds_to_global(o + 8, s_in, head, S);
-        } else {
-          flush_lds_to_global(o, s_out, 0, flen);
+          o[lane] = (uint8_t)(w >> (8u * (lane & 3u)));
         }
         if (lane == 0) { ret[v] = 0; frame_len[v] = flen; }
       }
@@ -387,11 +387,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
-  const bool small = max_len <= kSmallMax;
-  const uint32_t m = small ? kSmallMax : max_len;
-  const size_t in_bytes = in_region_bytes(small, m);
-  const size_t out_bytes = ((8u + (size_t)compress_bound(m) + 15u) & ~(size_t)15u) + 16u;
-  return kTableBytes + in_bytes + out_bytes;
+  const uint32_t m = max_len <= kSmallMax ? kSmallMax : max_len;
+  return kTableBytes + (((size_t)m + 15u) & ~(size_t)15u);
 }
 
 template <bool F, bool Sm>
