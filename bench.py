@@ -46,6 +46,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU leg")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--host-inclusive", action="store_true",
+                   help="also time pinned host -> device -> host (H2D + kernels + D2H, overlapped)")
+    p.add_argument("--hi-chunk", type=int, default=1 << 16, help="values per pipeline chunk")
+    p.add_argument("--hi-streams", type=int, default=4)
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="HBM traffic summary written by tools/pmc_traffic.py")
     return p.parse_args()
@@ -110,6 +114,39 @@ def cpu_baseline(sample: np.ndarray, size: int, seconds: float) -> dict:
     }
 
 
+def host_inclusive(batch, n: int, size: int, args) -> dict:
+    """Pinned host buffers -> H2D -> frame kernel -> pack -> D2H (ΣF bytes)
+    and back, chunked and overlapped over several streams (kingdb_amd/hostpipe.py).
+    Reported beside `value`, never as it."""
+    from kingdb_amd.hostpipe import HostPipeline
+    hp = HostPipeline(n, size, chunk=args.hi_chunk, nstreams=args.hi_streams)
+    hp.h_raw.np[:] = batch.src.download(n * size)
+    hp.compress()
+    hp.decompress()
+    tc, td = [], []
+    for _ in range(3):
+        tc.append(hp.compress())
+        td.append(hp.decompress())
+    cst, dst = hp.status()
+    ok = bool((cst == 0).all() and (dst == 0).all() and hp.frame_bytes == int(batch.frame_lens().astype(np.int64).sum())
+              and np.array_equal(hp.h_out.np, hp.h_raw.np))
+    if not ok:
+        raise SystemExit("bench: host-inclusive round trip is not bit-exact")
+    raw = float(n) * size
+    c, d = float(np.median(tc)), float(np.median(td))
+    res = {
+        "value": round(raw / (c + d) / GIB, 3), "unit": "GiB/s",
+        "compress_gibs": round(raw / c / GIB, 3), "decompress_gibs": round(raw / d / GIB, 3),
+        "compress_ms": round(c * 1e3, 3), "decompress_ms": round(d * 1e3, 3),
+        "pcie_bytes": {"compress_h2d": int(raw) + 20 * n, "compress_d2h": hp.frame_bytes + 8 * n,
+                       "decompress_h2d": hp.frame_bytes + 12 * n, "decompress_d2h": int(raw) + 8 * n},
+        "chunk": hp.chunk, "streams": len(hp.streams),
+        "timing": "host wall clock, first enqueue to last byte in pinned host memory; median of 3 after 1 warm-up",
+    }
+    hp.free()
+    return res
+
+
 def main() -> None:
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,6 +164,7 @@ def main() -> None:
 
     import kingdb_amd as K
     from kingdb_amd import lz4 as L
+    from kingdb_amd.shard import g1_first_piece, max_over_ranks
 
     K.set_device(local)
     torch_sync = torch.cuda.is_available()
@@ -144,7 +182,7 @@ def main() -> None:
 
     n, size = args.values, args.size
     stream = K.Stream()
-    first_piece = rank * ((n * size + 99) // 100)
+    first_piece = g1_first_piece(rank, n, size)  # rank's slice of one G1-long stream
     batch = K.DeviceBatch.g1_long(n, size, first_piece=first_piece, stream=stream)
     stream.sync()
 
@@ -167,10 +205,7 @@ def main() -> None:
     sync_all()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
 
     c_ms = float(np.mean([evs[k][0].elapsed_ms(evs[k][1]) for k in range(args.steps)]))
     d_ms = float(np.mean([evs[k][1].elapsed_ms(evs[k][2]) for k in range(args.steps)]))
@@ -187,13 +222,17 @@ def main() -> None:
     raw = float(n) * size
     frames = float(flen.sum())
     alg_bytes = raw + frames  # per launch, compress and decompress alike
-    dom_name, dom_ms = ("lz4_compress_kernel<true>", c_ms) if c_ms >= d_ms else ("lz4_decompress_kernel<true>", d_ms)
+    small = "true" if size <= 4096 else "false"
+    if c_ms >= d_ms:
+        dom_key, dom_name, dom_ms = "compress", f"kdb_lz4::lz4_compress_kernel<true, {small}>", c_ms
+    else:
+        dom_key, dom_name, dom_ms = "decompress", "kdb_lz4::lz4_decompress_kernel<true>", d_ms
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     try:
         pm = json.load(open(args.pmc))
-        if pm.get("values") == n and pm.get("size") == size and dom_name in pm.get("kernels", {}):
-            traffic = pm["kernels"][dom_name]["hbm_bytes_per_launch"]
+        if pm.get("values") == n and pm.get("size") == size:
+            traffic = pm["kernels"][dom_key]["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         pass
 
@@ -228,6 +267,8 @@ def main() -> None:
         "decompress_gibs": round(raw / (d_ms * 1e-3) / GIB, 2),
         "cpu_baseline": None,
     }
+    if args.host_inclusive:
+        line["host_inclusive"] = host_inclusive(batch, n, size, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ncpu = min(n, 131072)
         sample = batch.src.download(ncpu * size)

@@ -117,6 +117,15 @@ int kdb_lz4_decompress_frames_batch(void* stream, const uint8_t* src, const uint
                                     uint32_t max_out, uint8_t* dst, const uint64_t* dst_off,
                                     const uint32_t* dst_cap, uint32_t* out_len, int32_t* status);
 
+/* Compaction of frame slots into one dense stream (additive; the host-side
+ * equivalent is KingDB writing frames back to back: hstable_manager.h:656-673,
+ * database.cc:143-248).  dst_off[v] = exclusive prefix sum of len (device
+ * array), *total = Σ len (device pointer); frame v is copied from
+ * src + src_off[v] to dst + dst_off[v]. */
+int kdb_lz4_pack_frames(void* stream, const uint8_t* src, const uint64_t* src_off,
+                        const uint32_t* len, uint32_t n, uint8_t* dst, uint64_t* dst_off,
+                        uint64_t* total);
+
 /* ----------------------------------------------------------- data helpers */
 
 /* Synthetic G1 ("db_bench") data on the device: 100-byte pieces first_piece ..

@@ -56,6 +56,7 @@ SIGNATURES = {
     "kdb_lz4_decompress_blocks_batch": (_i, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
     "kdb_lz4_compress_frames_batch": (_i, [_vp, _vp, _vp, _vp, _u32, _u32, _vp, _vp, _vp, _vp]),
     "kdb_lz4_decompress_frames_batch": (_i, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "kdb_lz4_pack_frames": (_i, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "kdb_lz4_gen_g1": (_i, [_vp, _u64, _u64, _u32, _vp]),
     # link-time aliases of the reference's lz4.h names
     "LZ4_compressBound": (_i, [_i]),
