@@ -87,6 +87,35 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   const uint32_t b = a + lit;                                      // offset low byte
   const uint32_t total = has_match ? b + 2u + (long_ml ? nm + 1u : 0u) : b;
 #ifndef KDB_ABL_NO_EMIT
+  if (nl <= 6u && nm <= 5u) {
+    // Fast path: the header (token, literal-length run) and the trailer
+    // (offset, match-length run) are each <= 8 bytes, held as uniform 64-bit
+    // words and picked per lane with one v_perm_b32 (selector byte = index,
+    // clamped to 12 = "zero"); literals come from one LDS byte read.
+    const uint64_t hdr = (uint64_t)token |
+                         (lit >= kRunMask ? ((((1ull << (8u * nl)) - 1ull) << 8) | ((uint64_t)remL << (8u * (nl + 1u))))
+                                          : 0ull);
+    const uint64_t trl = (uint64_t)off |
+                         (long_ml ? ((((1ull << (8u * nm)) - 1ull) << 16) | ((uint64_t)remM << (8u * (nm + 2u)))) : 0ull);
+    const uint32_t h_lo = (uint32_t)hdr, h_hi = (uint32_t)(hdr >> 32);
+    const uint32_t t_lo = (uint32_t)trl, t_hi = (uint32_t)(trl >> 32);
+    const int lbase = (int)anchor - (int)a;
+#pragma unroll 1
+    for (uint32_t i = 0; i < total; i += 64u) {
+      const uint32_t j = i + lane;
+      const uint32_t lb = in[min(max(lbase + (int)j, 0), (int)S - 1)];
+      const uint32_t h = __builtin_amdgcn_perm(h_hi, h_lo, min(j, 12u) | 0x0C0C0C00u);
+      const uint32_t t = __builtin_amdgcn_perm(t_hi, t_lo, min(j - b, 12u) | 0x0C0C0C00u);
+      uint32_t val = j < a ? h : lb;
+      val = j >= b ? t : val;
+#ifdef KDB_ABL_SINK
+      asm volatile("" ::"v"(val), "v"(j < total ? 1u : 0u));
+#else
+      if (j < total && (!kGuard || pos + (int)j < out_cap)) out[pos + (int)j] = (uint8_t)val;
+#endif
+    }
+    return (int)total;
+  }
 #pragma unroll 1
   for (uint32_t i = 0; i < total; i += 64u) {
     const uint32_t j = i + lane;
@@ -105,19 +134,85 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
+// Unguarded output (the slot holds the bound): sequences are assembled in a
+// register ring -- lane l holds dword l of the pending 256-byte output window
+// -- and each window is written with ONE coalesced 64 x dword store when it
+// completes (plus a final partial store), instead of one wave-wide byte store
+// per sequence.  A sequence's bytes are computed per destination dword: lane l
+// of window w owns output bytes [256w + 4l, 256w + 4l + 4), literal bytes come
+// from one (clamped, realigned) LDS dword read.  Bytes past the block end are 0
+// and at most 3 of them are written (the slot's bound has >= 13 spare bytes).
+#ifndef KDB_RING
+#define KDB_RING 0
+#endif
+struct Ring {
+  uint32_t w;
+};
+
+__device__ __forceinline__ int emit_ring(uint8_t* __restrict__ out, int pos, Ring& rg, uint32_t token,
+                                         uint32_t lit, uint32_t nl, uint32_t remL, const uint8_t* in,
+                                         uint32_t S, uint32_t anchor, bool has_match, uint32_t off,
+                                         bool long_ml, uint32_t nm, uint32_t remM) {
+  const uint32_t lane = lane_id();
+  const uint32_t a = 1u + (lit >= kRunMask ? nl + 1u : 0u);      // first literal byte
+  const uint32_t b = a + lit;                                      // offset low byte
+  const uint32_t total = has_match ? b + 2u + (long_ml ? nm + 1u : 0u) : b;
+  const uint32_t end = (uint32_t)pos + total;
+  const int hi = (int)(S > 4u ? S : 4u) - 4;
+#ifndef KDB_ABL_NO_EMIT
+#pragma unroll 1
+  for (uint32_t w = (uint32_t)pos >> 8; (w << 8) < end; ++w) {
+    const int j0 = (int)((w << 8) + 4u * lane) - pos;
+    const int lp = (int)anchor + j0 - (int)a;
+    const int lpc = min(max(lp, 0), hi);
+    const uint32_t lw = lds_rd32(in, (uint32_t)lpc);
+    const int d = lp - lpc;
+    uint32_t nw = rg.w;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const uint32_t j = (uint32_t)(j0 + bb);                      // wraps negative -> huge
+      const uint32_t lb = (lw >> ((8 * (d + bb)) & 31)) & 255u;
+      const uint32_t rl = (j - 1u < nl) ? 255u : remL;
+      const uint32_t rm = (j - b - 2u < nm) ? 255u : remM;
+      uint32_t val = j == 0u ? token : j < a ? rl : j < b ? lb : j == b ? (off & 255u) : j == b + 1u ? (off >> 8) : rm;
+      const uint32_t sh = 8u * (uint32_t)bb;
+      nw = j < total ? ((nw & ~(255u << sh)) | (val << sh)) : nw;
+    }
+    rg.w = nw;
+    if ((w << 8) + 256u <= end) {                                   // window complete
+      reinterpret_cast<uint32_t*>(out + (w << 8))[lane] = nw;
+      rg.w = 0u;
+    }
+  }
+#endif
+  return (int)total;
+}
+
+// The last, partial window of a block of `n` bytes.
+__device__ __forceinline__ void ring_flush(uint8_t* __restrict__ out, uint32_t n, const Ring& rg) {
+  const uint32_t lane = lane_id();
+  const uint32_t tail = n & 255u;
+  if (tail && 4u * lane < tail) reinterpret_cast<uint32_t*>(out + (n & ~255u))[lane] = rg.w;
+}
+
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
 // points), like the reference.
 template <bool kTagged, bool kGuard>
-__device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const Table<kTagged>& tab,
+__device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const Table<kTagged>& tab,
                               uint8_t* __restrict__ out, int out_cap, int cap) {
   const uint32_t lane = lane_id();
   int op = 0;
   uint32_t anchor = 0;
+  Ring rg{0u};
 #define RD32(p) lds_rd32(in, (p))
 
+#ifdef KDB_ABL_NO_PARSE
+  if (S >= kMinLength && cap < 0) {
+#else
   if (S >= kMinLength) {                                    // lz4.cc:483
+#endif
     const uint32_t mflimit = S - kMfLimit;
     const uint32_t matchlimit = S - kLastLiterals;
     const uint32_t last4 = S - 4u;                          // highest position a u32 read may start
@@ -130,14 +225,19 @@ __device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const 
 #pragma unroll 1
       for (uint32_t kb = 0;; kb += 64u) {
         const uint32_t k = kb + lane;
-        const uint32_t pk = search_pos(s, k);
-        const bool valid = pk + search_step(k) <= mflimit;         // lz4.cc:510
+        // the first 65 iterations advance by 1 (step(k) = 1 for k <= 64)
+        const uint32_t pk = kb == 0 ? s + lane : search_pos(s, k);
+        const bool valid = pk + (kb == 0 ? 1u : search_step(k)) <= mflimit;   // lz4.cc:510
         const uint32_t seq = RD32(min(pk, last4));
         const uint32_t h = hash16(seq);
-        const uint32_t told = tab.get(h);
         const uint64_t vm = ballot(valid);
+        const uint32_t told = tab.get(h);
         // lanes of this chunk whose iteration hashes to the same slot
+        // (bit-sliced match-any: 13 ballots, overlapping the table read)
         uint32_t lo = ~0u, hi = ~0u;
+#ifdef KDB_ABL_NO_GROUP
+        lo = hi = 0u;
+#else
 #pragma unroll
         for (int bb = 0; bb < 13; ++bb) {
           const uint32_t t = (uint32_t)((int32_t)(h << (31 - bb)) >> 31);   // 0 or ~0
@@ -145,6 +245,7 @@ __device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const 
           lo &= ~(t ^ (uint32_t)m);
           hi &= ~(t ^ (uint32_t)(m >> 32));
         }
+#endif
         const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;
         const uint64_t below = same & mask_lt(lane);
         const uint32_t refk = below ? search_pos(s, kb + 63u - (uint32_t)__builtin_clzll(below)) : told;
@@ -159,7 +260,7 @@ __device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const 
           found = true;
           break;
         }
-        if (vm != ~0ull) break;              // ran past mflimit: last literals
+        if (vm != ~0ull) break;              // ran past mflimit: last literals (markers read as empty)
         if ((same & ~mask_le(lane)) == 0) tab.put(h, pk);
       }
       if (!found) break;
@@ -170,7 +271,11 @@ __device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const 
         // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
         uint32_t c, ml;
         {
+#ifdef KDB_ABL_NO_CATCH
+          const uint32_t lim = 0u;
+#else
           const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
+#endif
           const uint32_t rem = matchlimit - (ip + kMinMatch);
           const bool cl = lane < lim, ml_in = lane < rem;
           const uint32_t a0 = in[cl ? ip - 1u - lane : 0u], b0 = in[cl ? ref - 1u - lane : 0u];
@@ -214,8 +319,12 @@ __device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const 
         const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
         const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
         const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
-        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
+        if (kGuard || !KDB_RING)
+          op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
                                true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
+        else
+          op += emit_ring(out, op, rg, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
+                          true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
         ip = ip_end;
         anchor = ip;
         if (ip > mflimit) goto last_literals;                      // lz4.cc:597
@@ -227,7 +336,11 @@ __device__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const 
         if (lane == 0) tab.put(hash16(sm2), ip - 2u);
         const uint32_t r2 = uni(tab.get(hh));
         if (lane == 0) tab.put(hh, ip);
+#ifdef KDB_ABL_NO_NEXT
+        if (false) {
+#else
         if (r2 + kMaxDistance >= ip && RD32(r2) == sq) {
+#endif
           ref = r2;
           catchup = false;
           continue;                                                  // goto _next_match
@@ -243,8 +356,15 @@ last_literals:
     const uint32_t run = S - anchor;
     if (op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
     const uint32_t nl = run >= kRunMask ? (run - kRunMask) / 255u : 0u;
-    op += emit_seq<kGuard>(out, out_cap, op, (run >= kRunMask ? kRunMask : run) << 4, run, nl,
-                           run - kRunMask - 255u * nl, in, S, anchor, false, 0u, false, 0u, 0u);
+    const uint32_t tok = (run >= kRunMask ? kRunMask : run) << 4;
+    if (kGuard || !KDB_RING) {
+      op += emit_seq<kGuard>(out, out_cap, op, tok, run, nl, run - kRunMask - 255u * nl, in, S, anchor, false, 0u,
+                           false, 0u, 0u);
+    } else {
+      op += emit_ring(out, op, rg, tok, run, nl, run - kRunMask - 255u * nl, in, S, anchor, false, 0u, false, 0u,
+                      0u);
+      ring_flush(out, (uint32_t)op, rg);
+    }
   }
 #undef RD32
   return op;
@@ -364,7 +484,10 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
         const bool raw = (uint32_t)r > S;        // raw fallback (compressor.cc:40-48)
         const uint32_t stored = raw ? 0u : (uint32_t)r + 8u;
         const uint32_t flen = raw ? S + 8u : stored;
-        if (raw) flush_lds_to_global(o + 8, s_in, 0, S);
+        if (raw) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // block stores land before the raw bytes
+          flush_lds_to_global(o + 8, s_in, 0, S);
+        }
         if (lane < 8u) {                         // compressor.cc:53-54
           const uint32_t w = lane < 4u ? stored : S;
           o[lane] = (uint8_t)(w >> (8u * (lane & 3u)));

@@ -26,6 +26,13 @@ def test_kat_blocks_frames(gpu):
     fdec = gpu.decompress_frames(frames, [len(x) for x in inputs])
     for name, (st, out), x in zip(g["names"], fdec, inputs):
         assert st == 0 and out == x, name
+    # launches whose values are all <= 4 KiB take the tagged-table kernel
+    small = [i for i, x in enumerate(inputs) if len(x) <= 4096]
+    sin = [inputs[i] for i in small]
+    got = gpu.compress_blocks(sin)
+    for i, (r, b) in zip(small, got):
+        assert r == len(blocks[i]) and b == blocks[i], g["names"][i]
+    assert gpu.compress_frames(sin) == [frames[i] for i in small]
 
 
 def test_limited_output(gpu):
