@@ -145,6 +145,11 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
 #ifndef KDB_RING
 #define KDB_RING 0
 #endif
+#ifdef KDB_NO_SCHED
+#define SCHED_FENCE() ((void)0)
+#else
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#endif
 struct Ring {
   uint32_t w;
 };
@@ -217,23 +222,39 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
     const uint32_t matchlimit = S - kLastLiterals;
     const uint32_t last4 = S - 4u;                          // highest position a u32 read may start
     // lz4.cc:486: put(0) stores position 0 -- what an empty slot already reads as.
+    //
+    // The "test next position" step after a match (lz4.cc:600-618: get(ip),
+    // put(ip), compare; the distance check there always holds for byU16
+    // sizes) is a search iteration at ip without the skip counter, followed --
+    // when it fails -- by a fresh search from ip+1 whose first 65 iterations
+    // advance by 1.  So it runs as lane 0 of the next search chunk: positions
+    // ip, ip+1, ..., ip+63, lane 0 valid unconditionally (ip <= mflimit was
+    // checked), lanes >= 1 being search iterations 0..62.  A lane-0 match is
+    // _next_match: no catch-up, no literals.
     uint32_t s = 1;                                         // lz4.cc:487
+    uint32_t t0 = 0;                                        // 1: lane 0 of the first chunk is the test
     for (;;) {
       // ================= search (lz4.cc:494-527), 64 iterations per step
       uint32_t ip = 0, ref = 0;
-      bool found = false;
+      bool found = false, catchup = true;
 #pragma unroll 1
       for (uint32_t kb = 0;; kb += 64u) {
-        const uint32_t k = kb + lane;
-        // the first 65 iterations advance by 1 (step(k) = 1 for k <= 64)
-        const uint32_t pk = kb == 0 ? s + lane : search_pos(s, k);
-        const bool valid = pk + (kb == 0 ? 1u : search_step(k)) <= mflimit;   // lz4.cc:510
+        uint32_t pk;
+        bool valid;
+        if (kb == 0) {                               // step(k) = 1 for k <= 64
+          pk = s - t0 + lane;
+          valid = (lane < t0) || pk + 1u <= mflimit;   // lz4.cc:510
+        } else {
+          const uint32_t k = kb + lane - t0;
+          pk = search_pos(s, k);
+          valid = pk + search_step(k) <= mflimit;
+        }
         const uint32_t seq = RD32(min(pk, last4));
         const uint32_t h = hash16(seq);
-        const uint64_t vm = ballot(valid);
         const uint32_t told = tab.get(h);
+        const uint64_t vm = ballot(valid);
         // lanes of this chunk whose iteration hashes to the same slot
-        // (bit-sliced match-any: 13 ballots, overlapping the table read)
+        // (bit-sliced match-any: 13 ballots)
         uint32_t lo = ~0u, hi = ~0u;
 #ifdef KDB_ABL_NO_GROUP
         lo = hi = 0u;
@@ -248,106 +269,96 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
 #endif
         const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;
         const uint64_t below = same & mask_lt(lane);
-        const uint32_t refk = below ? search_pos(s, kb + 63u - (uint32_t)__builtin_clzll(below)) : told;
-        const bool match = valid && RD32(min(refk, last4)) == seq;   // lz4.cc:527
+        uint32_t refk = told;
+        if (below) {                                 // reference = the nearest earlier same-slot lane
+          const uint32_t jb = 63u - (uint32_t)__builtin_clzll(below);
+          refk = kb == 0 ? s - t0 + jb : search_pos(s, kb + jb - t0);
+        }
+        const bool match = valid && RD32(min(refk, last4)) == seq;   // lz4.cc:527, 610-616
         const uint64_t mm = ballot(match);
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
           const uint64_t later = same & ~mask_le(lane) & mask_le(ks);
-          if (valid && lane <= ks && later == 0) tab.put(h, pk);   // lz4.cc:526
+          if (valid && lane <= ks && later == 0) tab.put(h, pk);   // lz4.cc:526, 608
           ip = readlane(pk, ks);
           ref = readlane(refk, ks);
+          catchup = !(kb == 0 && ks < t0);
           found = true;
           break;
         }
-        if (vm != ~0ull) break;              // ran past mflimit: last literals (markers read as empty)
+        if (vm != ~0ull) break;              // ran past mflimit: last literals
         if ((same & ~mask_le(lane)) == 0) tab.put(h, pk);
       }
       if (!found) break;
 
-      bool catchup = true;
-#pragma unroll 1
-      for (;;) {  // one sequence per iteration; `continue` = _next_match with no literals
-        // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
-        uint32_t c, ml;
-        {
+      // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
+      uint32_t c, ml;
+      {
 #ifdef KDB_ABL_NO_CATCH
-          const uint32_t lim = 0u;
+        const uint32_t lim = 0u;
 #else
-          const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
+        const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
 #endif
-          const uint32_t rem = matchlimit - (ip + kMinMatch);
-          const bool cl = lane < lim, ml_in = lane < rem;
-          const uint32_t a0 = in[cl ? ip - 1u - lane : 0u], b0 = in[cl ? ref - 1u - lane : 0u];
-          const uint32_t a1 = in[ml_in ? ip + kMinMatch + lane : 0u];
-          const uint32_t b1 = in[ml_in ? ref + kMinMatch + lane : 0u];
-          c = first_zero(ballot(cl && a0 == b0));      // <= lim: lanes past it vote false
-          ml = first_zero(ballot(ml_in && a1 == b1));  // <= rem
-          if (c == 64u) {
+        const uint32_t rem = matchlimit - (ip + kMinMatch);
+        const bool cl = lane < lim, ml_in = lane < rem;
+        const uint32_t a0 = in[cl ? ip - 1u - lane : 0u], b0 = in[cl ? ref - 1u - lane : 0u];
+        const uint32_t a1 = in[ml_in ? ip + kMinMatch + lane : 0u];
+        const uint32_t b1 = in[ml_in ? ref + kMinMatch + lane : 0u];
+        c = first_zero(ballot(cl && a0 == b0));      // <= lim: lanes past it vote false
+        ml = first_zero(ballot(ml_in && a1 == b1));  // <= rem
+        if (c == 64u) {
 #pragma unroll 1
-            for (;;) {
-              const bool l2 = lane < lim - c;
-              const uint32_t x = in[l2 ? ip - c - 1u - lane : 0u], y = in[l2 ? ref - c - 1u - lane : 0u];
-              const uint32_t d = first_zero(ballot(l2 && x == y));
-              c += d;
-              if (d < 64u) break;
-            }
-          }
-          if (ml == 64u) {
-#pragma unroll 1
-            for (;;) {
-              const bool l2 = lane < rem - ml;
-              const uint32_t x = in[l2 ? ip + kMinMatch + ml + lane : 0u];
-              const uint32_t y = in[l2 ? ref + kMinMatch + ml + lane : 0u];
-              const uint32_t d = first_zero(ballot(l2 && x == y));
-              ml += d;
-              if (d < 64u) break;
-            }
+          for (;;) {
+            const bool l2 = lane < lim - c;
+            const uint32_t x = in[l2 ? ip - c - 1u - lane : 0u], y = in[l2 ? ref - c - 1u - lane : 0u];
+            const uint32_t d = first_zero(ballot(l2 && x == y));
+            c += d;
+            if (d < 64u) break;
           }
         }
-        const uint32_t ip_end = ip + kMinMatch + ml;  // independent of the catch-up
-        ip -= c;
-        ref -= c;
-        ml += c;
-
-        // ======== token + literals (lz4.cc:535-550), offset (554), match length (580-592)
-        const uint32_t lit = ip - anchor;
-        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 0;
-        const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
-        const bool long_ml = ml >= kMlMask;
-        if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
-        const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
-        const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
-        const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
-        if (kGuard || !KDB_RING)
-          op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
-                               true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
-        else
-          op += emit_ring(out, op, rg, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
-                          true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
-        ip = ip_end;
-        anchor = ip;
-        if (ip > mflimit) goto last_literals;                      // lz4.cc:597
-
-        // ======== fill table + test next position (lz4.cc:600-624)
-        const uint32_t sm2 = RD32(ip - 2u);
-        const uint32_t sq = RD32(ip);
-        const uint32_t hh = hash16(sq);
-        if (lane == 0) tab.put(hash16(sm2), ip - 2u);
-        const uint32_t r2 = uni(tab.get(hh));
-        if (lane == 0) tab.put(hh, ip);
-#ifdef KDB_ABL_NO_NEXT
-        if (false) {
-#else
-        if (r2 + kMaxDistance >= ip && RD32(r2) == sq) {
-#endif
-          ref = r2;
-          catchup = false;
-          continue;                                                  // goto _next_match
+        if (ml == 64u) {
+#pragma unroll 1
+          for (;;) {
+            const bool l2 = lane < rem - ml;
+            const uint32_t x = in[l2 ? ip + kMinMatch + ml + lane : 0u];
+            const uint32_t y = in[l2 ? ref + kMinMatch + ml + lane : 0u];
+            const uint32_t d = first_zero(ballot(l2 && x == y));
+            ml += d;
+            if (d < 64u) break;
+          }
         }
-        break;
       }
-      s = ip + 1u;                                                   // lz4.cc:623
+      const uint32_t ip_end = ip + kMinMatch + ml;  // independent of the catch-up
+      ip -= c;
+      ref -= c;
+      ml += c;
+
+      // ======== token + literals (lz4.cc:535-550), offset (554), match length (580-592)
+      const uint32_t lit = ip - anchor;
+      if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 0;
+      const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
+      const bool long_ml = ml >= kMlMask;
+      if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
+      const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
+      const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
+      const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
+      if (kGuard || !KDB_RING)
+        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
+                               true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
+      else
+        op += emit_ring(out, op, rg, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
+                        true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
+      ip = ip_end;
+      anchor = ip;
+      if (ip > mflimit) goto last_literals;                      // lz4.cc:597
+
+      // ======== fill table (lz4.cc:600); the test of ip is lane 0 of the next chunk
+      {
+        const uint32_t sm2 = RD32(ip - 2u);                     // same address in every lane
+        tab.put(hash16(sm2), ip - 2u);                          // identical stores: no conflict
+      }
+      s = ip + 1u;                                              // lz4.cc:623
+      t0 = 1u;
     }
   }
 
