@@ -39,7 +39,6 @@ inline int hip_status(hipError_t e) {
 }
 
 // Largest value the byU16 kernels take (lz4.cc:673: S < 65547).
-constexpr uint32_t kMaxKernelValue = k64KLimit - 1u;
 
 // Per-thread, per-device context of the scalar entry points.
 struct ScalarCtx {
@@ -151,7 +150,6 @@ int kdb_lz4_compressBound(int isize) { return (int)compress_bound((uint32_t)isiz
 int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize, int maxOutputSize) {
   if ((uint32_t)inputSize > kMaxInput) return 0;                 // lz4.cc:465
   if (maxOutputSize < 0) maxOutputSize = 0;
-  if ((uint32_t)inputSize > kMaxKernelValue) return 0;           // byU32 sizes: not in this build
   int err = 0;
   ScalarCtx& c = scalar_ctx(&err);
   if (err) return 0;
@@ -189,9 +187,7 @@ int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize
 
 int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compressedSize,
                                     int targetOutputSize, int maxDecompressedSize) {
-  // Sizes the kernel cannot take are reported like a malformed block at byte 0.
-  if (compressedSize < 0 || maxDecompressedSize < 0 || (uint32_t)maxDecompressedSize > kMaxKernelValue)
-    return -1;
+  if (compressedSize < 0 || maxDecompressedSize < 0) return -1;
   int err = 0;
   ScalarCtx& c = scalar_ctx(&err);
   if (err) return -1;
@@ -235,7 +231,6 @@ int kdb_lz4_compress_blocks_batch(void* stream, const uint8_t* src, const uint64
                                   const uint64_t* dst_off, const uint32_t* dst_cap, int32_t* ret) {
   if (n == 0) return KDB_LZ4_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !dst_cap || !ret) return KDB_LZ4_EINVAL;
-  if (max_len > kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
   return hip_status(launch_compress(false, (hipStream_t)stream, src, src_off, src_len, n, max_len, dst,
                                     dst_off, dst_cap, nullptr, ret));
 }
@@ -246,7 +241,6 @@ int kdb_lz4_decompress_blocks_batch(void* stream, const uint8_t* src, const uint
                                     const uint32_t* target, int32_t* ret) {
   if (n == 0) return KDB_LZ4_OK;
   if (!src || !src_off || !in_len || !dst || !dst_off || !dst_cap || !ret) return KDB_LZ4_EINVAL;
-  if (max_out > kMaxKernelValue || max_in > 2u * kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
   return hip_status(launch_decompress(false, (hipStream_t)stream, src, src_off, in_len, n, max_in, max_out,
                                       dst, dst_off, dst_cap, target, nullptr, ret));
 }
@@ -256,7 +250,6 @@ int kdb_lz4_compress_frames_batch(void* stream, const uint8_t* src, const uint64
                                   const uint64_t* dst_off, uint32_t* frame_len, int32_t* status) {
   if (n == 0) return KDB_LZ4_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !frame_len || !status) return KDB_LZ4_EINVAL;
-  if (max_len > kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
   return hip_status(launch_compress(true, (hipStream_t)stream, src, src_off, src_len, n, max_len, dst,
                                     dst_off, nullptr, frame_len, status));
 }
@@ -268,7 +261,6 @@ int kdb_lz4_decompress_frames_batch(void* stream, const uint8_t* src, const uint
   if (n == 0) return KDB_LZ4_OK;
   if (!src || !src_off || !avail || !dst || !dst_off || !dst_cap || !out_len || !status)
     return KDB_LZ4_EINVAL;
-  if (max_out > kMaxKernelValue || max_in > 2u * kMaxKernelValue) return KDB_LZ4_EUNSUPPORTED;
   return hip_status(launch_decompress(true, (hipStream_t)stream, src, src_off, avail, n, max_in, max_out,
                                       dst, dst_off, dst_cap, nullptr, out_len, status));
 }

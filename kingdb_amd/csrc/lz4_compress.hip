@@ -39,16 +39,21 @@ namespace kdb_lz4 {
 // Position visited at iteration k of a search run started at s (lz4.cc:497-507):
 // p(0)=s, p(k+1)=p(k)+step(k), step(0)=1, step(k)=(63+k)>>6 for k>=1, i.e.
 // p(k) = s + 1 + sum_{t=64}^{62+k} floor(t/64) for k >= 1.
+// (kWide: 64-bit intermediates -- a search can run ~500K iterations on 2 GB.)
+template <bool kWide>
 __device__ __forceinline__ uint32_t search_pos(uint32_t s, uint32_t k) {
   if (k == 0) return s;
   const uint32_t nn = 62u + k, q = nn >> 6, r = nn & 63u;
+  if (kWide) return (uint32_t)min((uint64_t)s + 1u + 32ull * q * (q - 1u) + (uint64_t)q * (r + 1u), 0xFFFFFFFFull);
   return s + 1u + 32u * q * (q - 1u) + q * (r + 1u);
 }
 __device__ __forceinline__ uint32_t search_step(uint32_t k) { return k == 0 ? 1u : (63u + k) >> 6; }
 
 __device__ __forceinline__ uint32_t hash16(uint32_t seq) { return (seq * 2654435761u) >> 19; }
+// lz4.cc:373-379: byU16 hashes to 13 bits, byU32 to 12
+template <bool kWide>
+__device__ __forceinline__ uint32_t hashp(uint32_t seq) { return (seq * 2654435761u) >> (kWide ? 20 : 19); }
 
-__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // The byU16 table.  kTagged: entry = gen << 12 | pos (values <= 4 KiB, so
 // positions < 4096); an entry of another generation is an empty slot (0).
@@ -66,6 +71,32 @@ struct Table {
   }
 };
 
+// byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
+struct Table32 {
+  uint32_t* t;
+  __device__ __forceinline__ uint32_t get(uint32_t h) const { return t[h]; }
+  __device__ __forceinline__ void put(uint32_t h, uint32_t p) const { t[h] = p; }
+};
+
+// Value bytes staged in LDS (byte i at p[i]).
+struct LdsSrc {
+  const uint8_t* p;
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t rd32(uint32_t i) const { return lds_rd32(p, i); }
+};
+
+// Value bytes read in place from global memory (any alignment).  An aligned
+// dword never lies on a page no needed byte lies on, so the reads cannot fault.
+struct GlobalSrc {
+  const uint8_t* g;
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const { return g[i]; }
+  __device__ __forceinline__ uint32_t rd32(uint32_t i) const {
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3u);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(g + i - mis);
+    return __builtin_amdgcn_alignbyte(w[mis ? 1 : 0], w[0], mis);
+  }
+};
+
 // Output: bytes go straight to HBM at out[0..).  kGuard (LZ4_compress_limitedOutput
 // with a caller cap below the bound): never write at or past out_cap -- the
 // reference may, on limitedOutput failures; the return value is what parity is
@@ -77,9 +108,9 @@ struct Table {
 // literals in[anchor .. anchor+lit), and -- when has_match -- the offset (LE16)
 // and the match-length run (nm bytes of 255 + remM, present iff long_ml).
 // One global_store_byte per 64 bytes.  Returns total.
-template <bool kGuard>
+template <bool kGuard, class Src>
 __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, int pos, uint32_t token,
-                                        uint32_t lit, uint32_t nl, uint32_t remL, const uint8_t* in,
+                                        uint32_t lit, uint32_t nl, uint32_t remL, const Src& src,
                                         uint32_t S, uint32_t anchor, bool has_match, uint32_t off,
                                         bool long_ml, uint32_t nm, uint32_t remM) {
   const uint32_t lane = lane_id();
@@ -103,7 +134,7 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
 #pragma unroll 1
     for (uint32_t i = 0; i < total; i += 64u) {
       const uint32_t j = i + lane;
-      const uint32_t lb = in[min(max(lbase + (int)j, 0), (int)S - 1)];
+      const uint32_t lb = src.u8((uint32_t)min(max(lbase + (int)j, 0), (int)S - 1));
       const uint32_t h = __builtin_amdgcn_perm(h_hi, h_lo, min(j, 12u) | 0x0C0C0C00u);
       const uint32_t t = __builtin_amdgcn_perm(t_hi, t_lo, min(j - b, 12u) | 0x0C0C0C00u);
       uint32_t val = j < a ? h : lb;
@@ -120,7 +151,7 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   for (uint32_t i = 0; i < total; i += 64u) {
     const uint32_t j = i + lane;
     const uint32_t li = min(anchor + (j - a), S - 1u);             // clamped LDS read
-    const uint32_t lb = in[(j >= a && j < b) ? li : 0u];
+    const uint32_t lb = src.u8((j >= a && j < b) ? li : 0u);
     uint32_t val;
     if (j == 0) val = token;
     else if (j < a) val = (j - 1u < nl) ? 255u : remL;
@@ -134,84 +165,18 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
-// Unguarded output (the slot holds the bound): sequences are assembled in a
-// register ring -- lane l holds dword l of the pending 256-byte output window
-// -- and each window is written with ONE coalesced 64 x dword store when it
-// completes (plus a final partial store), instead of one wave-wide byte store
-// per sequence.  A sequence's bytes are computed per destination dword: lane l
-// of window w owns output bytes [256w + 4l, 256w + 4l + 4), literal bytes come
-// from one (clamped, realigned) LDS dword read.  Bytes past the block end are 0
-// and at most 3 of them are written (the slot's bound has >= 13 spare bytes).
-#ifndef KDB_RING
-#define KDB_RING 0
-#endif
-#ifdef KDB_NO_SCHED
-#define SCHED_FENCE() ((void)0)
-#else
-#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-#endif
-struct Ring {
-  uint32_t w;
-};
-
-__device__ __forceinline__ int emit_ring(uint8_t* __restrict__ out, int pos, Ring& rg, uint32_t token,
-                                         uint32_t lit, uint32_t nl, uint32_t remL, const uint8_t* in,
-                                         uint32_t S, uint32_t anchor, bool has_match, uint32_t off,
-                                         bool long_ml, uint32_t nm, uint32_t remM) {
-  const uint32_t lane = lane_id();
-  const uint32_t a = 1u + (lit >= kRunMask ? nl + 1u : 0u);      // first literal byte
-  const uint32_t b = a + lit;                                      // offset low byte
-  const uint32_t total = has_match ? b + 2u + (long_ml ? nm + 1u : 0u) : b;
-  const uint32_t end = (uint32_t)pos + total;
-  const int hi = (int)(S > 4u ? S : 4u) - 4;
-#ifndef KDB_ABL_NO_EMIT
-#pragma unroll 1
-  for (uint32_t w = (uint32_t)pos >> 8; (w << 8) < end; ++w) {
-    const int j0 = (int)((w << 8) + 4u * lane) - pos;
-    const int lp = (int)anchor + j0 - (int)a;
-    const int lpc = min(max(lp, 0), hi);
-    const uint32_t lw = lds_rd32(in, (uint32_t)lpc);
-    const int d = lp - lpc;
-    uint32_t nw = rg.w;
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const uint32_t j = (uint32_t)(j0 + bb);                      // wraps negative -> huge
-      const uint32_t lb = (lw >> ((8 * (d + bb)) & 31)) & 255u;
-      const uint32_t rl = (j - 1u < nl) ? 255u : remL;
-      const uint32_t rm = (j - b - 2u < nm) ? 255u : remM;
-      uint32_t val = j == 0u ? token : j < a ? rl : j < b ? lb : j == b ? (off & 255u) : j == b + 1u ? (off >> 8) : rm;
-      const uint32_t sh = 8u * (uint32_t)bb;
-      nw = j < total ? ((nw & ~(255u << sh)) | (val << sh)) : nw;
-    }
-    rg.w = nw;
-    if ((w << 8) + 256u <= end) {                                   // window complete
-      reinterpret_cast<uint32_t*>(out + (w << 8))[lane] = nw;
-      rg.w = 0u;
-    }
-  }
-#endif
-  return (int)total;
-}
-
-// The last, partial window of a block of `n` bytes.
-__device__ __forceinline__ void ring_flush(uint8_t* __restrict__ out, uint32_t n, const Ring& rg) {
-  const uint32_t lane = lane_id();
-  const uint32_t tail = n & 255u;
-  if (tail && 4u * lane < tail) reinterpret_cast<uint32_t*>(out + (n & ~255u))[lane] = rg.w;
-}
-
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
 // points), like the reference.
-template <bool kTagged, bool kGuard>
-__device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, uint32_t S, const Table<kTagged>& tab,
-                              uint8_t* __restrict__ out, int out_cap, int cap) {
+template <bool kWide, bool kGuard, class Src, class Tab>
+__device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const Tab& tab,
+                                              uint8_t* __restrict__ out, int out_cap, int cap) {
+  constexpr int kHashBits = kWide ? 12 : 13;
   const uint32_t lane = lane_id();
   int op = 0;
   uint32_t anchor = 0;
-  Ring rg{0u};
-#define RD32(p) lds_rd32(in, (p))
+#define RD32(p) src.rd32(p)
 
 #ifdef KDB_ABL_NO_PARSE
   if (S >= kMinLength && cap < 0) {
@@ -239,18 +204,17 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
       bool found = false, catchup = true;
 #pragma unroll 1
       for (uint32_t kb = 0;; kb += 64u) {
-        uint32_t pk;
-        bool valid;
-        if (kb == 0) {                               // step(k) = 1 for k <= 64
-          pk = s - t0 + lane;
-          valid = (lane < t0) || pk + 1u <= mflimit;   // lz4.cc:510
-        } else {
-          const uint32_t k = kb + lane - t0;
-          pk = search_pos(s, k);
-          valid = pk + search_step(k) <= mflimit;
-        }
+        // positions: step(k) = 1 for k <= 64, so the first chunk is s-t0+lane
+        const uint32_t k = kb + lane - t0;
+        const uint32_t pk = kb == 0 ? s - t0 + lane : search_pos<kWide>(s, k);
+        const bool valid = (kb == 0 && lane < t0) || pk + (kb == 0 ? 1u : search_step(k)) <= mflimit;  // lz4.cc:510
         const uint32_t seq = RD32(min(pk, last4));
-        const uint32_t h = hash16(seq);
+        // lz4.cc:600 put(ip-2) of the previous sequence (ip = s-1): its read
+        // shares the round trip of the chunk's reads; the store precedes the
+        // chunk's table reads (in-order LDS)
+        const uint32_t sm2 = RD32(max(s, 3u) - 3u);
+        if (kb == 0 && t0) tab.put(hashp<kWide>(sm2), s - 3u);
+        const uint32_t h = hashp<kWide>(seq);
         const uint32_t told = tab.get(h);
         const uint64_t vm = ballot(valid);
         // lanes of this chunk whose iteration hashes to the same slot
@@ -260,7 +224,7 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
         lo = hi = 0u;
 #else
 #pragma unroll
-        for (int bb = 0; bb < 13; ++bb) {
+        for (int bb = 0; bb < kHashBits; ++bb) {
           const uint32_t t = (uint32_t)((int32_t)(h << (31 - bb)) >> 31);   // 0 or ~0
           const uint64_t m = ballot(t != 0u);
           lo &= ~(t ^ (uint32_t)m);
@@ -272,9 +236,11 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
         uint32_t refk = told;
         if (below) {                                 // reference = the nearest earlier same-slot lane
           const uint32_t jb = 63u - (uint32_t)__builtin_clzll(below);
-          refk = kb == 0 ? s - t0 + jb : search_pos(s, kb + jb - t0);
+          refk = kb == 0 ? s - t0 + jb : search_pos<kWide>(s, kb + jb - t0);
         }
-        const bool match = valid && RD32(min(refk, last4)) == seq;   // lz4.cc:527, 610-616
+        // byU32 adds the distance check (lz4.cc:526, 614); byU16 sizes never need it
+        const bool match = valid && (!kWide || refk + kMaxDistance >= pk) &&
+                           RD32(min(refk, last4)) == seq;   // lz4.cc:527, 610-616
         const uint64_t mm = ballot(match);
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
@@ -301,16 +267,16 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
 #endif
         const uint32_t rem = matchlimit - (ip + kMinMatch);
         const bool cl = lane < lim, ml_in = lane < rem;
-        const uint32_t a0 = in[cl ? ip - 1u - lane : 0u], b0 = in[cl ? ref - 1u - lane : 0u];
-        const uint32_t a1 = in[ml_in ? ip + kMinMatch + lane : 0u];
-        const uint32_t b1 = in[ml_in ? ref + kMinMatch + lane : 0u];
+        const uint32_t a0 = src.u8(cl ? ip - 1u - lane : 0u), b0 = src.u8(cl ? ref - 1u - lane : 0u);
+        const uint32_t a1 = src.u8(ml_in ? ip + kMinMatch + lane : 0u);
+        const uint32_t b1 = src.u8(ml_in ? ref + kMinMatch + lane : 0u);
         c = first_zero(ballot(cl && a0 == b0));      // <= lim: lanes past it vote false
         ml = first_zero(ballot(ml_in && a1 == b1));  // <= rem
         if (c == 64u) {
 #pragma unroll 1
           for (;;) {
             const bool l2 = lane < lim - c;
-            const uint32_t x = in[l2 ? ip - c - 1u - lane : 0u], y = in[l2 ? ref - c - 1u - lane : 0u];
+            const uint32_t x = src.u8(l2 ? ip - c - 1u - lane : 0u), y = src.u8(l2 ? ref - c - 1u - lane : 0u);
             const uint32_t d = first_zero(ballot(l2 && x == y));
             c += d;
             if (d < 64u) break;
@@ -320,8 +286,8 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
 #pragma unroll 1
           for (;;) {
             const bool l2 = lane < rem - ml;
-            const uint32_t x = in[l2 ? ip + kMinMatch + ml + lane : 0u];
-            const uint32_t y = in[l2 ? ref + kMinMatch + ml + lane : 0u];
+            const uint32_t x = src.u8(l2 ? ip + kMinMatch + ml + lane : 0u);
+            const uint32_t y = src.u8(l2 ? ref + kMinMatch + ml + lane : 0u);
             const uint32_t d = first_zero(ballot(l2 && x == y));
             ml += d;
             if (d < 64u) break;
@@ -335,28 +301,27 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
 
       // ======== token + literals (lz4.cc:535-550), offset (554), match length (580-592)
       const uint32_t lit = ip - anchor;
-      if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 0;
-      const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
       const bool long_ml = ml >= kMlMask;
-      if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
+      if (kGuard) {
+        // With cap >= compressBound these checks cannot fire (each sequence's
+        // encoding is at most its input + lit/255 bytes, so op stays below
+        // anchor + anchor/255 and both sides stay under the bound's 16 spare
+        // bytes); the unguarded instantiation omits them.
+        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 0;
+        const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
+        if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
+      }
       const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
       const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
       const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
-      if (kGuard || !KDB_RING)
-        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
-                               true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
-      else
-        op += emit_ring(out, op, rg, token, lit, nl, lit - kRunMask - 255u * nl, in, S, anchor,
-                        true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
+      op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, src, S, anchor,
+                             true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
       ip = ip_end;
       anchor = ip;
       if (ip > mflimit) goto last_literals;                      // lz4.cc:597
 
-      // ======== fill table (lz4.cc:600); the test of ip is lane 0 of the next chunk
-      {
-        const uint32_t sm2 = RD32(ip - 2u);                     // same address in every lane
-        tab.put(hash16(sm2), ip - 2u);                          // identical stores: no conflict
-      }
+      // the table fill of ip-2 (lz4.cc:600) and the test of ip (lane 0) run
+      // with the next chunk
       s = ip + 1u;                                              // lz4.cc:623
       t0 = 1u;
     }
@@ -365,17 +330,11 @@ __device__ __forceinline__ int compress_block(const uint8_t* __restrict__ in, ui
 last_literals:
   {  // lz4.cc:627-637
     const uint32_t run = S - anchor;
-    if (op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
+    if (kGuard && op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
     const uint32_t nl = run >= kRunMask ? (run - kRunMask) / 255u : 0u;
     const uint32_t tok = (run >= kRunMask ? kRunMask : run) << 4;
-    if (kGuard || !KDB_RING) {
-      op += emit_seq<kGuard>(out, out_cap, op, tok, run, nl, run - kRunMask - 255u * nl, in, S, anchor, false, 0u,
+    op += emit_seq<kGuard>(out, out_cap, op, tok, run, nl, run - kRunMask - 255u * nl, src, S, anchor, false, 0u,
                            false, 0u, 0u);
-    } else {
-      op += emit_ring(out, op, rg, tok, run, nl, run - kRunMask - 255u * nl, in, S, anchor, false, 0u, false, 0u,
-                      0u);
-      ring_flush(out, (uint32_t)op, rg);
-    }
   }
 #undef RD32
   return op;
@@ -420,7 +379,7 @@ __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint
 template <bool kFrame, bool kSmall>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t in_cap,
+    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
     int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
@@ -444,7 +403,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       const uint8_t* gp = src + src_off[w];
       p_head = uni((uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u));
       const uint4* base = reinterpret_cast<const uint4*>(gp - p_head);
-      p_chunks = uni((min(src_len[w], kSmallMax) + 15u) >> 4);
+      const uint32_t len = uni(src_len[w]);
+      p_chunks = (len >= min_len && len <= in_cap) ? (len + 15u) >> 4 : 0u;   // other launches' values: none
 #pragma unroll
       for (uint32_t i = 0; i < kPrefetch; ++i) {
         const uint32_t c = lane + 64u * i;
@@ -460,8 +420,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t S = uni(src_len[v]);
     const uint8_t* g = src + src_off[v];
     uint8_t* o = dst + dst_off[v];
-    if (S > in_cap || S >= k64KLimit) {             // byU32 sizes: not this kernel
-      if (lane == 0) { ret[v] = kUnsupported; if (kFrame) frame_len[v] = 0; }
+    if (S < min_len || S > in_cap) {             // another size class's launch owns it
       if (kSmall) prefetch(vn);
       v = vn;
       continue;
@@ -484,11 +443,11 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t bound = compress_bound(S);
     if (!kFrame) {
       const uint32_t cap = uni(dst_cap[v]);
-      const int r = cap < bound ? compress_block<kSmall, true>(s_in, S, tab, o, (int)cap, (int)cap)
-                                : compress_block<kSmall, false>(s_in, S, tab, o, (int)bound, (int)cap);
+      const int r = cap < bound ? compress_block<false, true>(LdsSrc{s_in}, S, tab, o, (int)cap, (int)cap)
+                                : compress_block<false, false>(LdsSrc{s_in}, S, tab, o, (int)bound, (int)cap);
       if (lane == 0) ret[v] = r;
     } else {
-      const int r = compress_block<kSmall, false>(s_in, S, tab, o + 8, (int)bound, (int)bound);
+      const int r = compress_block<false, false>(LdsSrc{s_in}, S, tab, o + 8, (int)bound, (int)bound);
       if (r <= 0) {                              // compressor.cc:31-34
         if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
       } else {
@@ -525,9 +484,79 @@ size_t compress_lds_bytes(uint32_t max_len) {
   return kTableBytes + (((size_t)m + 15u) & ~(size_t)15u);
 }
 
+// ---------------------------------------------------------------------------
+// Values of 65 547 bytes and more: LZ4_compress_generic(byU32) (lz4.cc:673-676;
+// 12-bit hash, u32 positions, distance check).  KingDB's default part size is
+// 1 MB (util/options.h:171), so whole parts land here.  The value is read in
+// place from global memory (L2), the 16 KiB table lives in LDS; one wave per
+// value.  Waves take 64 values at a time and compress the ones of this class.
+template <bool kFrame>
+__global__ __launch_bounds__(64) void lz4_compress_big_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint32_t n, uint8_t* __restrict__ dst,
+    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work) {
+  __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
+  const uint32_t lane = lane_id();
+  const Table32 tab{tab32};
+#pragma unroll 1
+  for (;;) {
+    uint32_t c0 = 0;
+    if (lane == 0) c0 = atomicAdd(work, 64u);
+    c0 = uni(c0);
+    if (c0 >= n) break;
+    const uint32_t vi = c0 + lane;
+    const uint32_t len = vi < n ? src_len[vi] : 0u;
+    uint64_t big = ballot(vi < n && len >= k64KLimit);
+#pragma unroll 1
+    while (big) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(big);
+      big &= big - 1ull;
+      const uint32_t v = c0 + l;
+      const uint32_t S = readlane(len, l);
+      const uint8_t* g = src + src_off[v];
+      uint8_t* o = dst + dst_off[v];
+      for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(0, 0, 0, 0);
+      const uint32_t bound = compress_bound(S);                   // 0 past LZ4_MAX_INPUT_SIZE
+      if (!kFrame) {
+        const uint32_t cap = uni(dst_cap[v]);
+        int r = 0;
+        if (bound != 0)
+          r = cap < bound ? compress_block<true, true>(GlobalSrc{g}, S, tab, o, (int)cap, (int)cap)
+                          : compress_block<true, false>(GlobalSrc{g}, S, tab, o, (int)bound, (int)cap);
+        if (lane == 0) ret[v] = r;
+      } else {
+        const int r = bound == 0 ? 0 : compress_block<true, false>(GlobalSrc{g}, S, tab, o + 8, (int)bound, (int)bound);
+        if (r <= 0) {                                             // compressor.cc:31-34
+          if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
+        } else {
+          const bool raw = (uint32_t)r > S;                       // compressor.cc:40-48
+          const uint32_t stored = raw ? 0u : (uint32_t)r + 8u;
+          if (raw) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll 1
+            for (uint32_t i = lane; i < S; i += 256u) {           // 4 loads in flight per lane
+              uint8_t b[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) b[k] = i + 64u * k < S ? g[i + 64u * k] : 0;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) if (i + 64u * k < S) o[8u + i + 64u * k] = b[k];
+            }
+          }
+          if (lane < 8u) {                                        // compressor.cc:53-54
+            const uint32_t w = lane < 4u ? stored : S;
+            o[lane] = (uint8_t)(w >> (8u * (lane & 3u)));
+          }
+          if (lane == 0) { ret[v] = 0; frame_len[v] = raw ? S + 8u : stored; }
+        }
+      }
+    }
+  }
+}
+
 template <bool F, bool Sm>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
-                             const uint32_t* src_len, uint32_t n, uint32_t in_cap, uint8_t* dst,
+                             const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret) {
   auto kern = lz4_compress_kernel<F, Sm>;
@@ -536,32 +565,58 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   if (e != hipSuccess) return e;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   const uint32_t batch = claim_batch(n, grid);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, in_cap, dst, dst_off,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch);
   return hipGetLastError();
 }
 
+template <bool F>
+static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                             uint32_t n, uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_cap,
+                             uint32_t* frame_len, int32_t* ret) {
+  auto kern = lz4_compress_big_kernel<F>;
+  uint32_t* work = nullptr;
+  hipError_t e = work_counter(st, &work);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, (n + 63u) / 64u);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, dst, dst_off, dst_cap, frame_len,
+                     ret, work);
+  return hipGetLastError();
+}
+
+// One launch per size class present up to max_len: <= 4 KiB (tagged table,
+// 20 KiB LDS: 8 values per CU), 4 KiB .. 65 546 B (LDS sized for the largest),
+// >= 65 547 B (byU32, in place).  Each launch skips the other classes' values.
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                            const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret) {
   if (n == 0) return hipSuccess;
-  const bool small = max_len <= kSmallMax;
-  const uint32_t in_cap = small ? kSmallMax : max_len;
-  size_t lds = compress_lds_bytes(max_len);
+  hipError_t e;
+  {
+    size_t lds = compress_lds_bytes(kSmallMax);
 #ifdef KDB_ABL_OCC
-  lds = 163840 / KDB_ABL_OCC;   // diagnostic: force KDB_ABL_OCC workgroups per CU
+    lds = 163840 / KDB_ABL_OCC;   // diagnostic: force KDB_ABL_OCC workgroups per CU
 #endif
-  if (frame) {
-    return small ? launch_one<true, true>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
-                                          frame_len, ret)
-                 : launch_one<true, false>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
-                                           frame_len, ret);
+    e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                       frame_len, ret)
+              : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                        frame_len, ret);
+    if (e != hipSuccess) return e;
   }
-  return small ? launch_one<false, true>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
-                                         frame_len, ret)
-               : launch_one<false, false>(st, lds, src, src_off, src_len, n, in_cap, dst, dst_off, dst_cap,
-                                          frame_len, ret);
+  if (max_len > kSmallMax) {
+    const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
+    const size_t lds = compress_lds_bytes(cap);
+    e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, cap, dst, dst_off,
+                                        dst_cap, frame_len, ret)
+              : launch_one<false, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, cap, dst, dst_off,
+                                         dst_cap, frame_len, ret);
+    if (e != hipSuccess) return e;
+  }
+  if (max_len >= k64KLimit)
+    e = frame ? launch_big<true>(st, src, src_off, src_len, n, dst, dst_off, dst_cap, frame_len, ret)
+              : launch_big<false>(st, src, src_off, src_len, n, dst, dst_off, dst_cap, frame_len, ret);
+  return e;
 }
 
 }  // namespace kdb_lz4

@@ -123,15 +123,14 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         asm volatile("" ::: "memory");
       }
     } else if (off > 0) {
-      // periodic: out[op+j] = out[ref + j mod off]   (j mod off via f32 reciprocal)
-      const float rcp = __builtin_amdgcn_rcpf((float)off);
+      // periodic: out[op+i+l] = out[ref + i + (l mod off)] -- the same byte as
+      // out[ref + (i+l) mod off], read from the step before (always written)
+      const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+      const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
         const int j = i + (int)lane;
-        const int qd = (int)(((float)i + lanef) * rcp);
-        int r = j - qd * off;
-        if (r >= off) r -= off;
-        const uint8_t b = out[ref + r];
+        const uint8_t b = out[ref + i + rr];
         if (j < mlen) out[op + j] = b;
       }
     }  // off == 0: the reference copies the destination onto itself
@@ -152,7 +151,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    uint32_t skip_big) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   const uint32_t out_bytes = ((out_cap_max + 15u) & ~15u) + 16u;
@@ -201,6 +201,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       tgt = target ? (int)uni(target[v]) : osize;
     }
     if ((uint32_t)csize > in_cap || (uint32_t)osize > out_cap_max || csize < 0 || osize < 0) {
+      // values too large for this launch's LDS: the ring decoder's (launched
+      // after it on the same stream) when skip_big, else unsupported
+      if (skip_big && csize >= 0 && osize >= 0) continue;
       if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
       continue;
     }
@@ -222,6 +225,288 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Values whose output exceeds what the LDS-resident decoder holds (> 65 546
+// bytes: KingDB's 1 MB parts, byU32 blocks) or whose block exceeds its staging
+// size.  Same decode rules (lz4.cc:876-1042); the value streams through two
+// LDS rings instead of being staged whole:
+//   * output: a 64 KiB ring -- every match source lies within 65 535 bytes --
+//     with each decoded byte also written straight to its place in HBM;
+//   * input: an 8 KiB ring refilled 4 KiB at a time from HBM (bytes at and
+//     past the block end staged as 0, like the zeroed tail of the LDS decoder),
+//     plus a 512-byte mirror of its start so the 256-byte register window
+//     never wraps.
+constexpr uint32_t kORing = 65536u, kOMask = kORing - 1u;
+constexpr uint32_t kIRing = 8192u, kIMask = kIRing - 1u, kIHalf = 4096u, kIMirror = 512u;
+constexpr size_t kRingLds = kORing + kIRing + kIMirror;
+
+struct InRing {
+  uint8_t* lds;          // kIRing + kIMirror bytes
+  const uint8_t* g;      // block start in HBM
+  uint32_t csize;
+  uint32_t filled;       // input bytes staged so far (multiple of kIHalf)
+
+  __device__ void refill() {
+    const uint32_t lane = lane_id();
+    const uint32_t rp = filled & kIMask;
+    uint32_t* r32 = reinterpret_cast<uint32_t*>(lds);
+#pragma unroll 4
+    for (uint32_t d = lane; d < kIHalf / 4u; d += 64u) {
+      const uint32_t P = filled + 4u * d;
+      uint32_t w = 0;
+      if (P < csize) {
+        // aligned dwords only: each covers a needed byte, so none can fault
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + P) & 3u);
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(g + P - mis);
+        const uint32_t lo = a[0];
+        const uint32_t hi = (mis != 0u && P + 4u - mis < csize) ? a[1] : 0u;
+        w = __builtin_amdgcn_alignbyte(hi, lo, mis);
+        const uint32_t have = csize - P;
+        if (have < 4u) w &= (1u << (8u * have)) - 1u;
+      }
+      r32[(rp >> 2) + d] = w;
+      if (rp == 0 && d < kIMirror / 4u) r32[kIRing / 4u + d] = w;
+    }
+    filled += kIHalf;
+  }
+  // bytes up to absolute input position `upto` staged (the oldest half is
+  // overwritten: callers only move forward, and never need bytes more than
+  // kIHalf behind the read position)
+  __device__ __forceinline__ bool ensure(uint32_t upto) {
+    bool any = false;
+    while (filled < upto) { refill(); any = true; }
+    return any;
+  }
+};
+
+// 256-byte register window over the input ring (ring coordinates).
+struct RingWindow {
+  const uint32_t* w32;
+  uint32_t base, win;
+  __device__ __forceinline__ void invalidate() { base = 0xFFFFFF00u; }
+  __device__ __forceinline__ uint32_t get4(uint32_t pos) {
+    const uint32_t p = uni(pos & kIMask);
+    if (p < base || p + 8u > base + 256u) {
+      base = uni(p & ~3u);
+      win = w32[(base >> 2) + lane_id()];
+    }
+    const uint32_t i = (p - base) >> 2;
+    const uint64_t q = ((uint64_t)readlane(win, i + 1u) << 32) | readlane(win, i);
+    return uni((uint32_t)(q >> (8u * (p & 3u))));
+  }
+};
+
+__device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __restrict__ o, int csize, int osize,
+                           int target) {
+  const uint32_t lane = lane_id();
+  const int iend = unii(csize), oend = unii(osize);
+  const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
+  RingWindow wd{reinterpret_cast<const uint32_t*>(in.lds), 0u, 0u};
+  wd.invalidate();
+  in.ensure(kIRing);
+  if (osize == 0) return (csize == 1 && (wd.get4(0) & 0xffu) == 0) ? 0 : -1;   // lz4.cc:911
+  const float lanef = (float)lane;
+  int ip = 0, op = 0;
+#pragma unroll 1
+  for (;;) {
+    ip = unii(ip);
+    op = unii(op);
+    if (in.ensure((uint32_t)ip + kIMirror)) wd.invalidate();
+    uint32_t q = wd.get4((uint32_t)ip);
+    const uint32_t token = q & 0xffu;
+    ip++;
+    int length = (int)(token >> 4);
+    if (length == (int)kRunMask) {                                // lz4.cc:917-925
+      uint32_t s = (q >> 8) & 0xffu;
+      ip++;
+      length += (int)s;
+#pragma unroll 1
+      while (ip < iend - (int)kRunMask && s == 255u) {
+        if (in.ensure((uint32_t)ip + kIMirror)) wd.invalidate();
+        s = wd.get4((uint32_t)ip) & 0xffu;
+        ip++;
+        length += (int)s;
+      }
+    }
+    const int cpy = op + length;                                  // lz4.cc:930-952
+    const bool last = cpy > oexit || ip + length > iend - (int)(2 + 1 + kLastLiterals);
+    if (last && (cpy > oend || ip + length > iend)) return -ip - 1;
+    // literals: from the input ring, in pieces of what is staged
+#pragma unroll 1
+    for (int done = 0; done < length;) {
+      if ((uint32_t)(ip + done) >= in.filled) { in.refill(); wd.invalidate(); }
+      const int piece = min(length - done, (int)(in.filled - (uint32_t)(ip + done)));
+#pragma unroll 1
+      for (int i = 0; i < piece; i += 64) {
+        const int j = i + (int)lane;
+        const uint8_t b = in.lds[(uint32_t)(ip + done + j) & kIMask];
+        if (j < piece) {
+          ring[(uint32_t)(op + done + j) & kOMask] = b;
+          o[op + done + j] = b;
+        }
+      }
+      done += piece;
+    }
+    ip += length;
+    op = cpy;
+    if (last) break;
+    if (in.ensure((uint32_t)ip + kIMirror)) wd.invalidate();
+    q = wd.get4((uint32_t)ip);                                    // offset (lz4.cc:955-956)
+    const int off = (int)(q & 0xffffu);
+    ip += 2;
+    const int ref = op - off;
+    if (ref < 0) return -ip - 1;
+    length = (int)(token & kMlMask);                              // lz4.cc:959-968
+    if (length == (int)kMlMask) {
+      if (ip > iend - (int)kLastLiterals) return -ip - 1;
+      uint32_t s = (q >> 16) & 0xffu;
+      ip++;
+      length += (int)s;
+#pragma unroll 1
+      while (s == 255u) {
+        if (ip > iend - (int)kLastLiterals) return -ip - 1;
+        if (in.ensure((uint32_t)ip + kIMirror)) wd.invalidate();
+        s = wd.get4((uint32_t)ip) & 0xffu;
+        ip++;
+        length += (int)s;
+      }
+    }
+    const int mlen = length + (int)kMinMatch;
+    if (op + mlen > oend - (int)kLastLiterals) return -ip - 1;    // lz4.cc:1024
+    asm volatile("" ::: "memory");
+    if (off >= mlen || off >= 64) {
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) {
+        const int j = i + (int)lane;
+        const uint8_t b = ring[(uint32_t)(ref + j) & kOMask];
+        if (j < mlen) {
+          ring[(uint32_t)(op + j) & kOMask] = b;
+          o[op + j] = b;
+        }
+        asm volatile("" ::: "memory");
+      }
+    } else if (off > 0) {
+      // periodic, sourced from the previous 64-byte step (never more than 64
+      // bytes behind, so never overwritten in the ring)
+      const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+      const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) {
+        const int j = i + (int)lane;
+        const uint8_t b = ring[(uint32_t)(ref + i + rr) & kOMask];
+        if (j < mlen) {
+          ring[(uint32_t)(op + j) & kOMask] = b;
+          o[op + j] = b;
+        }
+      }
+    } else {
+      // off == 0: the reference copies the destination onto itself (bytes it
+      // never wrote); the output is unspecified -- write the ring's bytes
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) {
+        const int j = i + (int)lane;
+        if (j < mlen) o[op + j] = ring[(uint32_t)(op + j) & kOMask];
+      }
+    }
+    asm volatile("" ::: "memory");
+    op += mlen;
+  }
+  return op;
+}
+
+// Values of this launch's class: out size > out_small or block > in_small.
+template <bool kFrame>
+__global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
+    const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = lane_id();
+  uint8_t* ring = smem;
+  uint8_t* iring = smem + kORing;
+#pragma unroll 1
+  for (;;) {
+    uint32_t c0 = 0;
+    if (lane == 0) c0 = atomicAdd(work, 64u);
+    c0 = uni(c0);
+    if (c0 >= n) break;
+    const uint32_t vi = c0 + lane;
+    bool mine = false;
+    if (vi < n) {
+      const uint32_t avail = in_len[vi];
+      uint32_t osz = out_cap[vi], csz = avail;
+      if (kFrame) {
+        const uint8_t* g = src + src_off[vi];
+        if (avail >= 8u) {
+          const uint32_t stored = (uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[2] << 16) | ((uint32_t)g[3] << 24);
+          const uint32_t raw = (uint32_t)g[4] | ((uint32_t)g[5] << 8) | ((uint32_t)g[6] << 16) | ((uint32_t)g[7] << 24);
+          osz = raw;
+          csz = stored - 8u;
+          // raw frames (stored == 0) are copied by the LDS launch at any size
+          mine = stored != 0 && raw <= out_cap[vi] && (osz > out_small || csz > in_small);
+        }
+      } else {
+        mine = osz > out_small || csz > in_small;
+      }
+    }
+    uint64_t todo = ballot(mine);
+#pragma unroll 1
+    while (todo) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1ull;
+      const uint32_t v = c0 + l;
+      const uint8_t* g = src + src_off[v];
+      uint8_t* o = dst + dst_off[v];
+      int csize, osize, tgt;
+      if (kFrame) {
+        const uint32_t stored =
+            uni((uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[2] << 16) | ((uint32_t)g[3] << 24));
+        const uint32_t raw =
+            uni((uint32_t)g[4] | ((uint32_t)g[5] << 8) | ((uint32_t)g[6] << 16) | ((uint32_t)g[7] << 24));
+        const uint32_t avail = uni(in_len[v]);
+        if (stored == 0) {                                        // raw frame (compressor.cc:116-124)
+          if (raw + 8u > avail) {
+            if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+            continue;
+          }
+          for (uint32_t i = lane; i < raw; i += 64u) o[i] = g[8u + i];
+          if (lane == 0) { ret[v] = 0; out_len[v] = raw; }
+          continue;
+        }
+        csize = (int)(stored - 8u);
+        osize = (int)raw;
+        tgt = osize;
+        g += 8;
+        if (csize < 0 || (uint32_t)csize + 8u > avail) {
+          if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+          continue;
+        }
+      } else {
+        csize = (int)uni(in_len[v]);
+        osize = (int)uni(out_cap[v]);
+        tgt = target ? (int)uni(target[v]) : osize;
+        if (csize < 0 || osize < 0) {
+          if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
+          continue;
+        }
+      }
+      InRing in{iring, g, (uint32_t)csize, 0u};
+      const int r = decode_ring(in, ring, o, csize, osize, tgt);
+      if (lane == 0) {
+        if (kFrame) {
+          ret[v] = r > 0 ? 0 : -1;
+          out_len[v] = r > 0 ? (uint32_t)r : 0u;
+        } else {
+          ret[v] = r;
+          if (out_len) out_len[v] = r > 0 ? (uint32_t)r : 0u;
+        }
+      }
+    }
+  }
+}
+
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
   // out window | staged block + zero tail + the register window's 256-byte reach
   return (((size_t)max_out + 15u) & ~(size_t)15u) + 16u + (((size_t)max_in + 15u) & ~(size_t)15u) + 320u;
@@ -231,7 +516,7 @@ template <bool F>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
-                             uint32_t* out_len, int32_t* ret) {
+                             uint32_t* out_len, int32_t* ret, uint32_t skip_big) {
   auto kern = lz4_decompress_kernel<F>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
@@ -239,20 +524,45 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
-                     out_cap, target, out_len, ret, work, batch);
+                     out_cap, target, out_len, ret, work, batch, skip_big);
   return hipGetLastError();
 }
+
+template <bool F>
+static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
+                             uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst, const uint64_t* dst_off,
+                             const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
+  auto kern = lz4_decompress_big_kernel<F>;
+  uint32_t* work = nullptr;
+  hipError_t e = work_counter(st, &work);
+  if (e != hipSuccess) return e;
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), kRingLds, (n + 63u) / 64u);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), kRingLds, st, src, src_off, in_len, n, in_small, out_small, dst,
+                     dst_off, out_cap, target, out_len, ret, work);
+  return hipGetLastError();
+}
+
+// LDS-resident decoder for outputs up to 65 546 bytes (blocks up to the bound
+// of that, plus a frame header); the ring decoder after it for the rest.
+constexpr uint32_t kOutSmallMax = k64KLimit - 1u;
+constexpr uint32_t kInSmallMax = kOutSmallMax + kOutSmallMax / 255u + 16u + 8u;
 
 hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
                              uint8_t* dst, const uint64_t* dst_off, const uint32_t* out_cap,
                              const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   if (n == 0) return hipSuccess;
-  const size_t lds = decompress_lds_bytes(max_in, max_out);
-  return frame ? launch_one<true>(st, lds, src, src_off, in_len, n, max_in, max_out, dst, dst_off, out_cap,
-                                  target, out_len, ret)
-               : launch_one<false>(st, lds, src, src_off, in_len, n, max_in, max_out, dst, dst_off, out_cap,
-                                   target, out_len, ret);
+  const bool big = max_out > kOutSmallMax || max_in > kInSmallMax;
+  const uint32_t mi = max_in < kInSmallMax ? max_in : kInSmallMax;
+  const uint32_t mo = max_out < kOutSmallMax ? max_out : kOutSmallMax;
+  const size_t lds = decompress_lds_bytes(mi, mo);
+  hipError_t e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
+                                          out_len, ret, big ? 1u : 0u)
+                       : launch_one<false>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
+                                           out_len, ret, big ? 1u : 0u);
+  if (e != hipSuccess || !big) return e;
+  return frame ? launch_big<true>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
+               : launch_big<false>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
 }
 
 }  // namespace kdb_lz4

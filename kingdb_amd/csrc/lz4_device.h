@@ -40,6 +40,8 @@ __device__ __forceinline__ uint32_t readlane(uint32_t x, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
 
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 // Lanes-below / lanes-up-to masks (lane in 0..63; 2ull<<63 wraps to 0 -> ~0).
 __device__ __forceinline__ uint64_t mask_lt(uint32_t l) { return (1ull << l) - 1ull; }
 __device__ __forceinline__ uint64_t mask_le(uint32_t l) { return (2ull << l) - 1ull; }

@@ -19,7 +19,6 @@ import numpy as np
 
 from . import _lib
 
-MAX_KERNEL_VALUE = 65536 + 10  # byU16 range (lz4.cc:673: S < 65547)
 
 
 def lib():

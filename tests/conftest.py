@@ -47,3 +47,32 @@ def gpu():
         pytest.fail("no GPU visible to libkdb_lz4.so")
     kingdb_amd.set_device(0)
     return kingdb_amd
+
+
+def big_value_inputs(g, pool_bytes):
+    """Inputs of big_values.npz by name: G1 pool slices and 'a' runs are
+    regenerated (tests/golden/make_golden.py:big_inputs), the rest stored."""
+    out = []
+    for name, size in zip(g["names"], g["sizes"]):
+        name, size = str(name), int(size)
+        if name.startswith("g1_"):
+            start = 7 if size == 100000 else 0
+            out.append(pool_bytes[start:start + size])
+        elif name.startswith("a_"):
+            out.append(b"a" * size)
+        else:
+            out.append(g["inp_" + name].tobytes())
+        assert len(out[-1]) == size, name
+    return out
+
+
+def apply_recipe(blk, kind, pos, val):
+    """kind 0: truncate to pos bytes; 1: flip bit val at pos; 2: set pos to val."""
+    b = bytearray(blk)
+    if kind == 0:
+        return bytes(b[:pos])
+    if kind == 1:
+        b[pos] ^= 1 << val
+    else:
+        b[pos] = val
+    return bytes(b)

@@ -189,7 +189,70 @@ def main() -> None:
     np.savez_compressed(os.path.join(OUT, "test_compression.npz"),
                         frames=np.frombuffer(stream, np.uint8).copy(),
                         frame_len=np.array([len(f) for f in frms], np.int64))
+    # ---- 7. values past the byU16 range (byU32 encoder, ring decoder):
+    #         KingDB's default part size is 1 MB (util/options.h:171).
+    big = big_inputs(ref, pool)
+    b_names = [k for k, _ in big]
+    b_frames = [ref.frame(v) for _, v in big]
+    b_blocks = [ref.compress(v) for _, v in big]
+    keep_inp = {k: np.frombuffer(v, np.uint8).copy() for k, v in big if not k.startswith(("g1_", "a_"))}
+    arrs = {f"inp_{k}": v for k, v in keep_inp.items()}
+    arrs["names"] = np.array(b_names)
+    arrs["sizes"] = np.array([len(v) for _, v in big], np.int64)
+    arrs["frm_len"] = np.array([len(f) for f in b_frames], np.int64)
+    arrs["frm_crc"] = np.array([ref.crc32c(f) for f in b_frames], np.int64)
+    arrs["blk_len"] = np.array([len(b) for b in b_blocks], np.int64)
+    arrs["blk_crc"] = np.array([ref.crc32c(b) for b in b_blocks], np.int64)
+    # malformed big blocks: truncations / byte edits of the 1 MiB G1 block,
+    # kept as recipes (kind, position, value) applied by the test to the block
+    # the GPU produced (itself pinned by length + crc above)
+    rng = random.Random(5)
+    base_blk = b_blocks[b_names.index("g1_1048576")]
+    recipes, m_ret = [], []
+    for it in range(12):
+        kind = it % 3
+        pos = rng.randrange(1, len(base_blk)) if kind == 0 else rng.randrange(len(base_blk))
+        val = rng.randrange(8) if kind == 1 else 0xFF
+        blk = apply_recipe(base_blk, kind, pos, val)
+        r, _ = ref_decode(ref, blk, 1 << 20, 1 << 20)
+        recipes.append((kind, pos, val))
+        m_ret.append(r)
+    arrs["mal_recipe"] = np.array(recipes, np.int64)
+    arrs["mal_ret"] = np.array(m_ret, np.int64)
+    np.savez_compressed(os.path.join(OUT, "big_values.npz"), **arrs)
+    print("big values:", list(zip(b_names, arrs["frm_len"].tolist())), "malformed rets", m_ret)
     print("fixtures written to", OUT)
+
+
+def apply_recipe(blk: bytes, kind: int, pos: int, val: int) -> bytes:
+    """kind 0: truncate to pos bytes; 1: flip bit val at pos; 2: set pos to val."""
+    b = bytearray(blk)
+    if kind == 0:
+        return bytes(b[:pos])
+    if kind == 1:
+        b[pos] ^= 1 << val
+    else:
+        b[pos] = val
+    return bytes(b)
+
+
+def big_inputs(ref: oracle.Reference, pool: np.ndarray) -> list[tuple[str, bytes]]:
+    """Inputs >= 65 547 bytes.  g1_* and a_* are regenerated by the tests
+    (G1 pool slices, 'a' runs); the others are stored in the fixture."""
+    g1 = pool.tobytes()
+    g2 = ref.g2(300000, 1).tobytes()
+    g3 = ref.g3(200000, 1).tobytes()
+    text = (b"the quick brown fox jumps over the lazy dog 0123456789 " * 10000)[:500000]
+    return [
+        ("g1_65547", g1[:65547]),
+        ("g1_100000", g1[7:100007]),
+        ("g1_262144", g1[:262144]),
+        ("g1_1048576", g1[:1048576]),
+        ("a_1048576", b"a" * 1048576),
+        ("g2_300000", g2),
+        ("g3_200000", g3),
+        ("text_500000", text),
+    ]
 
 
 def ref_decode(ref: oracle.Reference, blk: bytes, size: int, tgt: int):

@@ -214,3 +214,47 @@ def test_host_pipeline(gpu, orc):
     assert (dst == 0).all()
     assert np.array_equal(hp.h_out.np, hp.h_raw.np)
     hp.free()
+
+
+def test_big_values_byu32(gpu, orc):
+    """>= 65 547 B values (byU32 kernel + ring decoder), alone and mixed with
+    small ones in the same launch (one launch per size class)."""
+    from conftest import apply_recipe, big_value_inputs
+    g = load_golden("big_values.npz")
+    inputs = big_value_inputs(g, oracle.g1_pool(orc).tobytes())
+    frames = gpu.compress_frames(inputs)
+    blocks = gpu.compress_blocks(inputs)
+    for name, x, f, (r, b), fl, fc, bl, bc in zip(g["names"], inputs, frames, blocks, g["frm_len"], g["frm_crc"],
+                                                   g["blk_len"], g["blk_crc"]):
+        assert len(f) == int(fl) and orc.crc32c(f) == int(fc), name
+        assert r == int(bl) and orc.crc32c(b) == int(bc), name
+    back = gpu.decompress_frames(frames, [len(x) for x in inputs])
+    for name, (st, out), x in zip(g["names"], back, inputs):
+        assert st == 0 and out == x, name
+    dec = gpu.decompress_blocks([b for _, b in blocks], [len(x) for x in inputs])
+    for name, (r, out), x in zip(g["names"], dec, inputs):
+        assert r == len(x) and out == x, name
+    # malformed 1 MiB blocks: exact return codes
+    base = dict(zip([str(n) for n in g["names"]], [b for _, b in blocks]))["g1_1048576"]
+    mal = [apply_recipe(base, int(k), int(p), int(v)) for k, p, v in g["mal_recipe"]]
+    got = gpu.decompress_blocks(mal, [1 << 20] * len(mal))
+    for (r, _), ret in zip(got, g["mal_ret"]):
+        assert r == int(ret)
+    # one mixed launch: 100 B .. 1 MiB
+    pool = oracle.g1_pool(orc)
+    mixed = []
+    for i, x in enumerate(inputs):
+        mixed += oracle.g1_values(pool, 100, 3) + [x] + oracle.g1_values(pool, 4096, 2) + [x[: 5000 + i]]
+    mf = gpu.compress_frames(mixed)
+    assert mf == [orc.frame(x) for x in mixed]
+    mb = gpu.decompress_frames(mf, [len(x) for x in mixed])
+    assert all(st == 0 and out == x for (st, out), x in zip(mb, mixed))
+
+
+def test_big_scalar_mirrors(gpu, orc):
+    pool = oracle.g1_pool(orc).tobytes()
+    x = pool[:300000]
+    r, b = gpu.compress_limited_output(x, gpu.compress_bound(len(x)))
+    assert b == orc.compress(x)
+    r2, out = gpu.decompress_safe_partial(b, len(x), len(x))
+    assert r2 == len(x) and out == x

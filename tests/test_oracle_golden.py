@@ -94,3 +94,24 @@ def test_g1_generator_jump_ahead_matches_sequential(orc):
             s = s * A % M
             raw.append(32 + s % 95)
         assert bytes(raw * 2) == seq[j * 100:(j + 1) * 100].tobytes()
+
+
+def test_big_values_byu32(orc):
+    """Values past the byU16 range (>= 65 547 B: byU32 encoder) and the
+    malformed-block codes on a 1 MiB block, against the reference's digests."""
+    from conftest import apply_recipe, big_value_inputs
+    g = load_golden("big_values.npz")
+    inputs = big_value_inputs(g, oracle.g1_pool(orc).tobytes())
+    blocks = {}
+    for name, x, fl, fc, bl, bc in zip(g["names"], inputs, g["frm_len"], g["frm_crc"], g["blk_len"], g["blk_crc"]):
+        f = orc.frame(x)
+        b = orc.compress(x)
+        assert len(f) == int(fl) and orc.crc32c(f) == int(fc), name
+        assert len(b) == int(bl) and orc.crc32c(b) == int(bc), name
+        r, out = orc.decompress(b, len(x))
+        assert r == len(x) and out == x, name
+        blocks[str(name)] = b
+    base = blocks["g1_1048576"]
+    for (kind, pos, val), ret in zip(g["mal_recipe"], g["mal_ret"]):
+        r, _ = orc.decompress(apply_recipe(base, int(kind), int(pos), int(val)), 1 << 20)
+        assert r == int(ret), (kind, pos, val)
