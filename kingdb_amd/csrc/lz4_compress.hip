@@ -118,48 +118,23 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   const uint32_t b = a + lit;                                      // offset low byte
   const uint32_t total = has_match ? b + 2u + (long_ml ? nm + 1u : 0u) : b;
 #ifndef KDB_ABL_NO_EMIT
-  if (nl <= 6u && nm <= 5u) {
-    // Fast path: the header (token, literal-length run) and the trailer
-    // (offset, match-length run) are each <= 8 bytes, held as uniform 64-bit
-    // words and picked per lane with one v_perm_b32 (selector byte = index,
-    // clamped to 12 = "zero"); literals come from one LDS byte read.
-    const uint64_t hdr = (uint64_t)token |
-                         (lit >= kRunMask ? ((((1ull << (8u * nl)) - 1ull) << 8) | ((uint64_t)remL << (8u * (nl + 1u))))
-                                          : 0ull);
-    const uint64_t trl = (uint64_t)off |
-                         (long_ml ? ((((1ull << (8u * nm)) - 1ull) << 16) | ((uint64_t)remM << (8u * (nm + 2u)))) : 0ull);
-    const uint32_t h_lo = (uint32_t)hdr, h_hi = (uint32_t)(hdr >> 32);
-    const uint32_t t_lo = (uint32_t)trl, t_hi = (uint32_t)(trl >> 32);
-    const int lbase = (int)anchor - (int)a;
-#pragma unroll 1
-    for (uint32_t i = 0; i < total; i += 64u) {
-      const uint32_t j = i + lane;
-      const uint32_t lb = src.u8((uint32_t)min(max(lbase + (int)j, 0), (int)S - 1));
-      const uint32_t h = __builtin_amdgcn_perm(h_hi, h_lo, min(j, 12u) | 0x0C0C0C00u);
-      const uint32_t t = __builtin_amdgcn_perm(t_hi, t_lo, min(j - b, 12u) | 0x0C0C0C00u);
-      uint32_t val = j < a ? h : lb;
-      val = j >= b ? t : val;
-#ifdef KDB_ABL_SINK
-      asm volatile("" ::"v"(val), "v"(j < total ? 1u : 0u));
-#else
-      if (j < total && (!kGuard || pos + (int)j < out_cap)) out[pos + (int)j] = (uint8_t)val;
-#endif
-    }
-    return (int)total;
-  }
-#pragma unroll 1
+  // One pass per 64 bytes; every byte class is a compare-select: token,
+  // 255-run bytes, remL, literals (one LDS byte read), offset, 255-run, remM.
+  const uint32_t remL_at = lit >= kRunMask ? a - 1u : 0xFFFFFFFFu;     // 0 is the token
+  const uint32_t remM_at = long_ml ? total - 1u : 0xFFFFFFFFu;
+  const int lbase = (int)anchor - (int)a;
+#pragma clang loop unroll(disable)
   for (uint32_t i = 0; i < total; i += 64u) {
     const uint32_t j = i + lane;
-    const uint32_t li = min(anchor + (j - a), S - 1u);             // clamped LDS read
-    const uint32_t lb = src.u8((j >= a && j < b) ? li : 0u);
-    uint32_t val;
-    if (j == 0) val = token;
-    else if (j < a) val = (j - 1u < nl) ? 255u : remL;
-    else if (j < b) val = lb;
-    else if (j == b) val = off & 255u;
-    else if (j == b + 1u) val = off >> 8;
-    else val = (j - b - 2u < nm) ? 255u : remM;
+    const uint32_t lb = src.u8((uint32_t)min(max(lbase + (int)j, 0), (int)S - 1));
+    const uint32_t h = j == 0 ? token : (j == remL_at ? remL : 255u);
+    const uint32_t t = j == b ? (off & 255u) : j == b + 1u ? (off >> 8) : (j == remM_at ? remM : 255u);
+    const uint32_t val = j < a ? h : (j < b ? lb : t);
+#ifdef KDB_ABL_SINK
+    asm volatile("" ::"v"(val), "v"(j < total ? 1u : 0u));
+#else
     if (j < total && (!kGuard || pos + (int)j < out_cap)) out[pos + (int)j] = (uint8_t)val;
+#endif
   }
 #endif
   return (int)total;
