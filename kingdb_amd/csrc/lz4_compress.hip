@@ -202,8 +202,9 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         for (int bb = 0; bb < kHashBits; ++bb) {
           const uint32_t t = (uint32_t)((int32_t)(h << (31 - bb)) >> 31);   // 0 or ~0
           const uint64_t m = ballot(t != 0u);
-          lo &= ~(t ^ (uint32_t)m);
-          hi &= ~(t ^ (uint32_t)(m >> 32));
+          // acc & ~(t ^ m) in one v_bitop3 per half (truth table 0x90)
+          lo = __builtin_amdgcn_bitop3_b32(lo, t, (uint32_t)m, 0x90);
+          hi = __builtin_amdgcn_bitop3_b32(hi, t, (uint32_t)(m >> 32), 0x90);
         }
 #endif
         const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;
