@@ -151,6 +151,11 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
   const uint32_t lane = lane_id();
   int op = 0;
   uint32_t anchor = 0;
+  // A sequence of <= 64 encoded bytes is written at the top of the next
+  // chunk: its literal read shares that chunk's first LDS round trip and its
+  // selects and store fill the wait (unguarded mode only).
+  int pe_pos = 0, pe_lbase = 0;
+  uint32_t pe_a = 0, pe_b = 0, pe_total = 0, pe_w0 = 0, pe_w1 = 0;   // w0 = tok|remL<<8|remM<<16, w1 = off
 #define RD32(p) src.rd32(p)
 
 #ifdef KDB_ABL_NO_PARSE
@@ -188,6 +193,17 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         // shares the round trip of the chunk's reads; the store precedes the
         // chunk's table reads (in-order LDS)
         const uint32_t sm2 = RD32(max(s, 3u) - 3u);
+        if (!kGuard) {                               // the pending sequence
+          const uint32_t j = lane;
+          const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
+          const uint32_t h = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
+          const uint32_t t = j == pe_b ? (pe_w1 & 255u)
+                           : j == pe_b + 1u ? (pe_w1 >> 8)
+                           : (j + 1u == pe_total ? (pe_w0 >> 16) : 255u);
+          const uint32_t val = j < pe_a ? h : (j < pe_b ? lb : t);
+          if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
+          pe_total = 0;
+        }
         if (kb == 0 && t0) tab.put(hashp<kWide>(sm2), s - 3u);
         const uint32_t h = hashp<kWide>(seq);
         const uint32_t told = tab.get(h);
@@ -290,8 +306,22 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
       const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
       const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
       const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
-      op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, lit - kRunMask - 255u * nl, src, S, anchor,
-                             true, ip - ref, long_ml, nm, ml - kMlMask - 255u * nm);
+      const uint32_t remL = lit - kRunMask - 255u * nl, remM = ml - kMlMask - 255u * nm;
+      const uint32_t ea = 1u + (lit >= kRunMask ? nl + 1u : 0u);
+      const uint32_t etot = ea + lit + 2u + (long_ml ? nm + 1u : 0u);
+      if (!kGuard && etot <= 64u) {
+        pe_pos = op;
+        pe_lbase = (int)anchor - (int)ea;
+        pe_a = ea;
+        pe_b = ea + lit;
+        pe_total = etot;
+        pe_w0 = token | ((lit >= kRunMask ? remL : 0u) << 8) | ((long_ml ? remM : 0u) << 16);
+        pe_w1 = ip - ref;
+        op += (int)etot;
+      } else {
+        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, remL, src, S, anchor, true, ip - ref, long_ml,
+                               nm, remM);
+      }
       ip = ip_end;
       anchor = ip;
       if (ip > mflimit) goto last_literals;                      // lz4.cc:597
@@ -304,6 +334,16 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
   }
 
 last_literals:
+  if (!kGuard && pe_total) {                       // the last pending sequence
+    const uint32_t j = lane;
+    const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
+    const uint32_t h = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
+    const uint32_t t = j == pe_b ? (pe_w1 & 255u)
+                     : j == pe_b + 1u ? (pe_w1 >> 8)
+                     : (j + 1u == pe_total ? (pe_w0 >> 16) : 255u);
+    const uint32_t val = j < pe_a ? h : (j < pe_b ? lb : t);
+    if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
+  }
   {  // lz4.cc:627-637
     const uint32_t run = S - anchor;
     if (kGuard && op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
