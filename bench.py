@@ -43,6 +43,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--values", type=int, default=1 << 20, help="values per GPU")
     p.add_argument("--size", type=int, default=4096, help="bytes per value")
+    p.add_argument("--workload", choices=("uniform", "mixed"), default="uniform",
+                   help="uniform: --values x --size (configs[2], the headline); mixed: configs[3], "
+                        "--values per GPU of 90%% 100 B / 9%% 4 KiB / 1%% 64 KiB parts, byte-balanced shards")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU leg")
     p.add_argument("--no-verify", action="store_true")
@@ -182,8 +185,18 @@ def main() -> None:
 
     n, size = args.values, args.size
     stream = K.Stream()
-    first_piece = g1_first_piece(rank, n, size)  # rank's slice of one G1-long stream
-    batch = K.DeviceBatch.g1_long(n, size, first_piece=first_piece, stream=stream)
+    if args.workload == "mixed":
+        # configs[3]: one global mixed batch of n*world values, byte-balanced
+        # contiguous shards; each rank generates its own slice.
+        from kingdb_amd.shard import byte_balanced_ranges
+        gsizes = L.mixed_sizes(n * world)
+        lo, hi = byte_balanced_ranges(gsizes, world)[rank]
+        before = int(gsizes[:lo].astype(np.int64).sum())
+        batch = K.DeviceBatch.g1_long_sizes(gsizes[lo:hi], first_piece=(before + 99) // 100, stream=stream)
+        n = batch.n
+    else:
+        first_piece = g1_first_piece(rank, n, size)  # rank's slice of one G1-long stream
+        batch = K.DeviceBatch.g1_long(n, size, first_piece=first_piece, stream=stream)
     stream.sync()
 
     for _ in range(args.warmup):
@@ -213,30 +226,37 @@ def main() -> None:
     # correctness of what was timed (outside the timed region)
     cst, dst = batch.status()
     flen = batch.frame_lens().astype(np.int64)
-    ok = bool((cst == 0).all() and (dst == 0).all() and (batch.out_lens() == size).all())
+    ok = bool((cst == 0).all() and (dst == 0).all() and np.array_equal(batch.out_lens(), batch.sizes))
     if ok and not args.no_verify:
-        ok = bool(np.array_equal(batch.src.download(n * size), batch.out.download(n * size)))
+        ok = batch.roundtrip_ok()
     if not ok:
         raise SystemExit("bench: round trip is not bit-exact -- refusing to report a number")
 
-    raw = float(n) * size
+    raw = float(batch.raw_bytes)
     frames = float(flen.sum())
     alg_bytes = raw + frames  # per launch, compress and decompress alike
-    small = "true" if size <= 4096 else "false"
-    if c_ms >= d_ms:
-        dom_key, dom_name, dom_ms = "compress", f"kdb_lz4::lz4_compress_kernel<true, {small}>", c_ms
+    if args.workload == "mixed":
+        # several size-class launches per step: the roofline covers the step's launches together
+        kc, kd = "all compress launches of the step", "all decompress launches of the step"
     else:
-        dom_key, dom_name, dom_ms = "decompress", "kdb_lz4::lz4_decompress_kernel<true>", d_ms
+        kc = ("kdb_lz4::lz4_compress_kernel<true, true>" if size <= 4096 else
+              "kdb_lz4::lz4_compress_big_kernel<true, false>" if size < 65547 else
+              "kdb_lz4::lz4_compress_big_kernel<true, true>")
+        kd = "kdb_lz4::lz4_decompress_kernel<true>" if size <= 8192 else "kdb_lz4::lz4_decompress_big_kernel<true, 4096u>"
+    if c_ms >= d_ms:
+        dom_key, dom_name, dom_ms = "compress", kc, c_ms
+    else:
+        dom_key, dom_name, dom_ms = "decompress", kd, d_ms
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
     try:
         pm = json.load(open(args.pmc))
-        if pm.get("values") == n and pm.get("size") == size:
+        if args.workload == "uniform" and pm.get("values") == n and pm.get("size") == size:
             traffic = pm["kernels"][dom_key]["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         pass
 
-    total_raw = raw * world * args.steps
+    total_raw = max_over_ranks(raw, op="sum") * args.steps
     value = total_raw / elapsed / GIB
     line = {
         "metric": METRIC,
@@ -252,8 +272,14 @@ def main() -> None:
         "dtype": "u8",
         "data": "synthetic: G1-long (db_bench CompressibleString 0.5, LevelDB Random(301)), generated on device",
         "config": {
-            "workload": f"{n} x {size} B values per GPU: CompressorLZ4 frame compress + frame decompress (round trip)",
-            "values_per_gpu": n, "value_bytes": size, "parallelism": f"dp{world} (independent shards, no collective)",
+            "workload": (f"{n} x {size} B values per GPU: CompressorLZ4 frame compress + frame decompress (round trip)"
+                         if args.workload == "uniform" else
+                         f"configs[3] mixed batch, {n} values on rank 0 (by count 90% 100 B / 9% 4 KiB / 1% 64 KiB "
+                         f"parts, {args.values * world} values byte-balanced over {world} GPU(s)): frame compress + "
+                         f"frame decompress (round trip)"),
+            "values_per_gpu": n, "value_bytes": size if args.workload == "uniform" else "mixed",
+            "raw_bytes_per_gpu": int(raw),
+            "parallelism": f"dp{world} (independent shards, no collective)",
             "ratio": round(frames / raw, 4),
         },
         "roofline": {
@@ -267,9 +293,9 @@ def main() -> None:
         "decompress_gibs": round(raw / (d_ms * 1e-3) / GIB, 2),
         "cpu_baseline": None,
     }
-    if args.host_inclusive:
+    if args.host_inclusive and args.workload == "uniform":
         line["host_inclusive"] = host_inclusive(batch, n, size, args)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "uniform":
         ncpu = min(n, 131072)
         sample = batch.src.download(ncpu * size)
         line["cpu_baseline"] = cpu_baseline(sample, size, args.cpu_seconds)

@@ -32,6 +32,9 @@
 //    together: the match length after catching up c bytes is c + the length
 //    measured from the original position, so neither waits for the other;
 //  * the byte emission of a sequence.
+#include <cstdlib>
+#include <type_traits>
+
 #include "lz4_device.h"
 
 namespace kdb_lz4 {
@@ -357,6 +360,7 @@ last_literals:
 }
 
 constexpr uint32_t kSmallMax = 4096u;     // tagged table + register prefetch
+constexpr uint32_t kMidLdsMax = 8192u;    // LDS-staged values up to here, in place above
 constexpr uint32_t kPrefetch = 4u;        // output chunks per lane: 4096 / 16 / 64
 
 // out chunk = bytes [sh, sh+16) of the 32 bytes (a, b); sh in 0..15 (uniform)
@@ -505,25 +509,30 @@ size_t compress_lds_bytes(uint32_t max_len) {
 // 12-bit hash, u32 positions, distance check).  KingDB's default part size is
 // 1 MB (util/options.h:171), so whole parts land here.  The value is read in
 // place from global memory (L2), the 16 KiB table lives in LDS; one wave per
-// value.  Waves take 64 values at a time and compress the ones of this class.
-template <bool kFrame>
+// value.  Waves claim up to 16 values at a time and compress the ones of this class.
+template <bool kFrame, bool kWide>
 __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const uint32_t* __restrict__ src_len, uint32_t n, uint8_t* __restrict__ dst,
-    const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work) {
+    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
   const uint32_t lane = lane_id();
-  const Table32 tab{tab32};
+  // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
+  using Tab = typename std::conditional<kWide, Table32, Table<false>>::type;
+  Tab tab;
+  if constexpr (kWide) tab = Table32{tab32};
+  else tab = Table<false>{reinterpret_cast<uint16_t*>(tab32), 0u};
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
-    if (lane == 0) c0 = atomicAdd(work, 64u);
+    if (lane == 0) c0 = atomicAdd(work, batch);
     c0 = uni(c0);
     if (c0 >= n) break;
     const uint32_t vi = c0 + lane;
-    const uint32_t len = vi < n ? src_len[vi] : 0u;
-    uint64_t big = ballot(vi < n && len >= k64KLimit);
+    const bool in_claim = lane < batch && vi < n;
+    const uint32_t len = in_claim ? src_len[vi] : 0u;
+    uint64_t big = ballot(in_claim && len >= min_len && len <= max_len);
 #pragma unroll 1
     while (big) {
       const uint32_t l = (uint32_t)__builtin_ctzll(big);
@@ -538,11 +547,11 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
         const uint32_t cap = uni(dst_cap[v]);
         int r = 0;
         if (bound != 0)
-          r = cap < bound ? compress_block<true, true>(GlobalSrc{g}, S, tab, o, (int)cap, (int)cap)
-                          : compress_block<true, false>(GlobalSrc{g}, S, tab, o, (int)bound, (int)cap);
+          r = cap < bound ? compress_block<kWide, true>(GlobalSrc{g}, S, tab, o, (int)cap, (int)cap)
+                          : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o, (int)bound, (int)cap);
         if (lane == 0) ret[v] = r;
       } else {
-        const int r = bound == 0 ? 0 : compress_block<true, false>(GlobalSrc{g}, S, tab, o + 8, (int)bound, (int)bound);
+        const int r = bound == 0 ? 0 : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o + 8, (int)bound, (int)bound);
         if (r <= 0) {                                             // compressor.cc:31-34
           if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
         } else {
@@ -586,17 +595,18 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   return hipGetLastError();
 }
 
-template <bool F>
+template <bool F, bool W>
 static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
-                             uint32_t n, uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_cap,
-                             uint32_t* frame_len, int32_t* ret) {
-  auto kern = lz4_compress_big_kernel<F>;
+                             uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst, const uint64_t* dst_off,
+                             const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret) {
+  auto kern = lz4_compress_big_kernel<F, W>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
   if (e != hipSuccess) return e;
-  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, (n + 63u) / 64u);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, dst, dst_off, dst_cap, frame_len,
-                     ret, work);
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
+  const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
+                     dst_cap, frame_len, ret, work, batch);
   return hipGetLastError();
 }
 
@@ -620,18 +630,35 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                                         frame_len, ret);
     if (e != hipSuccess) return e;
   }
-  if (max_len > kSmallMax) {
-    const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
-    const size_t lds = compress_lds_bytes(cap);
-    e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, cap, dst, dst_off,
+  // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
+  // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
+  // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
+  static const uint32_t mid_split = [] {
+    const char* e = getenv("KDB_LZ4_CSPLIT");
+    return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : kMidLdsMax;
+  }();
+  if (max_len > kSmallMax && mid_split > kSmallMax) {
+    const uint32_t hi = min(min(max_len, mid_split), k64KLimit - 1u);
+    const size_t lds = compress_lds_bytes(hi);
+    e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
                                         dst_cap, frame_len, ret)
-              : launch_one<false, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, cap, dst, dst_off,
+              : launch_one<false, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
                                          dst_cap, frame_len, ret);
     if (e != hipSuccess) return e;
   }
+  const uint32_t glo = max(mid_split, kSmallMax) + 1u;
+  if (max_len >= glo && glo < k64KLimit) {
+    const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
+    e = frame ? launch_big<true, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len, ret)
+              : launch_big<false, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
+                                         ret);
+    if (e != hipSuccess) return e;
+  }
   if (max_len >= k64KLimit)
-    e = frame ? launch_big<true>(st, src, src_off, src_len, n, dst, dst_off, dst_cap, frame_len, ret)
-              : launch_big<false>(st, src, src_off, src_len, n, dst, dst_off, dst_cap, frame_len, ret);
+    e = frame ? launch_big<true, true>(st, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
+                                       frame_len, ret)
+              : launch_big<false, true>(st, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
+                                        frame_len, ret);
   return e;
 }
 

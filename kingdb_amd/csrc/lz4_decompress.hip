@@ -21,6 +21,7 @@
 // out[ref + (i mod offset)] -- every source byte is already final and one pass
 // suffices (the same bytes as the reference's dec32/dec64 copy, lz4.cc:1008-1018).
 #include <cstdio>
+#include <cstdlib>
 
 #include "lz4_device.h"
 
@@ -236,9 +237,9 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
 //     past the block end staged as 0, like the zeroed tail of the LDS decoder),
 //     plus a 512-byte mirror of its start so the 256-byte register window
 //     never wraps.
-constexpr uint32_t kORing = 65536u, kOMask = kORing - 1u;
 constexpr uint32_t kIRing = 8192u, kIMask = kIRing - 1u, kIHalf = 4096u, kIMirror = 512u;
-constexpr size_t kRingLds = kORing + kIRing + kIMirror;
+template <uint32_t kORing>
+constexpr size_t ring_lds() { return kORing + kIRing + kIMirror; }
 
 struct InRing {
   uint8_t* lds;          // kIRing + kIMirror bytes
@@ -296,8 +297,10 @@ struct RingWindow {
   }
 };
 
+template <uint32_t kORing>
 __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __restrict__ o, int csize, int osize,
                            int target) {
+  constexpr uint32_t kOMask = kORing - 1u;
   const uint32_t lane = lane_id();
   const int iend = unii(csize), oend = unii(osize);
   const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
@@ -374,7 +377,22 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
     const int mlen = length + (int)kMinMatch;
     if (op + mlen > oend - (int)kLastLiterals) return -ip - 1;    // lz4.cc:1024
     asm volatile("" ::: "memory");
-    if (off >= mlen || off >= 64) {
+    if ((uint32_t)off > kORing) {
+      // the source left the ring: read it back from this wave's own output in
+      // HBM (ordered after the stores by a workgroup-scope release/acquire)
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int j = i + (int)lane;
+        const uint8_t b = j < mlen ? o[ref + j] : (uint8_t)0;
+        if (j < mlen) {
+          ring[(uint32_t)(op + j) & kOMask] = b;
+          o[op + j] = b;
+        }
+        asm volatile("" ::: "memory");
+      }
+    } else if (off >= mlen || off >= 64) {
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
         const int j = i + (int)lane;
@@ -415,13 +433,13 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
 }
 
 // Values of this launch's class: out size > out_small or block > in_small.
-template <bool kFrame>
+template <bool kFrame, uint32_t kORing>
 __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work) {
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   uint8_t* ring = smem;
@@ -429,12 +447,12 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
-    if (lane == 0) c0 = atomicAdd(work, 64u);
+    if (lane == 0) c0 = atomicAdd(work, batch);
     c0 = uni(c0);
     if (c0 >= n) break;
     const uint32_t vi = c0 + lane;
     bool mine = false;
-    if (vi < n) {
+    if (lane < batch && vi < n) {
       const uint32_t avail = in_len[vi];
       uint32_t osz = out_cap[vi], csz = avail;
       if (kFrame) {
@@ -493,7 +511,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
         }
       }
       InRing in{iring, g, (uint32_t)csize, 0u};
-      const int r = decode_ring(in, ring, o, csize, osize, tgt);
+      const int r = decode_ring<kORing>(in, ring, o, csize, osize, tgt);
       if (lane == 0) {
         if (kFrame) {
           ret[v] = r > 0 ? 0 : -1;
@@ -528,41 +546,74 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   return hipGetLastError();
 }
 
-template <bool F>
+template <bool F, uint32_t R>
 static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
                              uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst, const uint64_t* dst_off,
                              const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
-  auto kern = lz4_decompress_big_kernel<F>;
+  auto kern = lz4_decompress_big_kernel<F, R>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
   if (e != hipSuccess) return e;
-  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), kRingLds, (n + 63u) / 64u);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), kRingLds, st, src, src_off, in_len, n, in_small, out_small, dst,
-                     dst_off, out_cap, target, out_len, ret, work);
+  const size_t lds = ring_lds<R>();
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
+                     dst_off, out_cap, target, out_len, ret, work, batch);
   return hipGetLastError();
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* e = getenv(name);
+  return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : dflt;
+}
+
+template <bool F>
+static hipError_t launch_ring(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
+                              uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst, const uint64_t* dst_off,
+                              const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
+  static const uint32_t ring = env_u32("KDB_LZ4_ORING", 4096u);
+  switch (ring) {
+    case 8192u:
+      return launch_big<F, 8192u>(st, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                  out_len, ret);
+    case 16384u:
+      return launch_big<F, 16384u>(st, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                  out_len, ret);
+    case 32768u:
+      return launch_big<F, 32768u>(st, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                   out_len, ret);
+    case 65536u:
+      return launch_big<F, 65536u>(st, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                   out_len, ret);
+    default:
+      return launch_big<F, 4096u>(st, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                   out_len, ret);
+  }
 }
 
 // LDS-resident decoder for outputs up to 65 546 bytes (blocks up to the bound
 // of that, plus a frame header); the ring decoder after it for the rest.
 constexpr uint32_t kOutSmallMax = k64KLimit - 1u;
-constexpr uint32_t kInSmallMax = kOutSmallMax + kOutSmallMax / 255u + 16u + 8u;
 
 hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
                              uint8_t* dst, const uint64_t* dst_off, const uint32_t* out_cap,
                              const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   if (n == 0) return hipSuccess;
-  const bool big = max_out > kOutSmallMax || max_in > kInSmallMax;
-  const uint32_t mi = max_in < kInSmallMax ? max_in : kInSmallMax;
-  const uint32_t mo = max_out < kOutSmallMax ? max_out : kOutSmallMax;
+  // LDS-resident decoder up to `split` output bytes, the ring decoder above
+  static const uint32_t split = min(env_u32("KDB_LZ4_DSPLIT", 8192u), kOutSmallMax);
+  const uint32_t in_split = split + split / 255u + 16u + 8u;
+  const bool big = max_out > split || max_in > in_split;
+  const uint32_t mi = max_in < in_split ? max_in : in_split;
+  const uint32_t mo = max_out < split ? max_out : split;
   const size_t lds = decompress_lds_bytes(mi, mo);
   hipError_t e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
                                           out_len, ret, big ? 1u : 0u)
                        : launch_one<false>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
                                            out_len, ret, big ? 1u : 0u);
   if (e != hipSuccess || !big) return e;
-  return frame ? launch_big<true>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
-               : launch_big<false>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
+  return frame ? launch_ring<true>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
+               : launch_ring<false>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
 }
 
 }  // namespace kdb_lz4

@@ -292,53 +292,91 @@ def decompress_frames(frames: list[bytes], sizes: list[int]) -> list[tuple[int, 
 
 
 # ------------------------------------------------------ device-resident batch
+# the mixed batch, by count 90% 100 B values, 9% 4 KiB
+# values and 1% 64 KiB parts (network/server.cc:258 cuts 64 KiB parts).
+MIX_CONFIG4 = ((100, 0.90), (4096, 0.09), (65536, 0.01))
+
+
+def mixed_sizes(n: int, mix=MIX_CONFIG4, seed: int = 4) -> np.ndarray:
+    """n value sizes with the given by-count mix, in a seeded shuffled order
+    (the exact counts are round(n * share), the remainder going to the first class)."""
+    counts = [int(round(n * f)) for _, f in mix]
+    counts[0] += n - sum(counts)
+    sizes = np.concatenate([np.full(c, sz, np.uint32) for (sz, _), c in zip(mix, counts)])
+    np.random.default_rng(seed).shuffle(sizes)
+    return sizes
+
+
 @dataclass
 class DeviceBatch:
-    """A batch of n equal-size values resident in HBM, with frame slots and the
-    metadata arrays the kernels take.  Used by bench.py and the large parity
-    tests; nothing here touches host memory after construction."""
+    """A batch of n values resident in HBM (sizes may differ per value), with
+    frame slots and the metadata arrays the kernels take.  Values are packed
+    back to back in `src`; decoded values land at the same offsets in `out`.
+    Used by bench.py and the large parity tests; nothing here touches host
+    memory after construction."""
 
     n: int
-    size: int
+    size: int                  # largest value size of the batch
+    sizes: np.ndarray          # u32 per value
+    src_off: np.ndarray        # u64 per value (same offsets in `out`)
+    frame_off: np.ndarray      # u64 per value (16-aligned frame slots)
     src: DeviceBuffer
     frames: DeviceBuffer
     out: DeviceBuffer
     meta: DeviceBuffer
-    slot: int
+    slot: int                  # largest frame slot
+
+    @property
+    def raw_bytes(self) -> int:
+        return int(self.sizes.astype(np.int64).sum())
 
     @classmethod
     def g1_long(cls, n: int, size: int, first_piece: int = 0, stream: Stream | None = None) -> "DeviceBatch":
         """n consecutive `size`-byte slices of the G1-long pool (piece-aligned start)."""
-        total = n * size
+        return cls.g1_long_sizes(np.full(n, size, np.uint32), first_piece=first_piece, stream=stream)
+
+    @classmethod
+    def g1_long_sizes(cls, sizes: np.ndarray, first_piece: int = 0, stream: Stream | None = None) -> "DeviceBatch":
+        """Values of the given sizes, consecutive slices of the G1-long pool."""
+        sizes = np.asarray(sizes, dtype=np.uint32)
+        total = int(sizes.astype(np.int64).sum())
         npieces = (total + 99) // 100
         src = DeviceBuffer(npieces * 100 + 64)
         st = stream.ptr if stream else None
         _lib.check(lib().kdb_lz4_gen_g1(src.ptr, first_piece, npieces, 301, st), "gen_g1")
-        return cls._layout(n, size, src, stream)
+        return cls._layout(sizes, src, stream)
 
     @classmethod
     def from_host(cls, values: np.ndarray, size: int, stream: Stream | None = None) -> "DeviceBatch":
         n = values.nbytes // size
         src = DeviceBuffer(values.nbytes + 64)
         src.upload(values)
-        return cls._layout(n, size, src, stream)
+        return cls._layout(np.full(n, size, np.uint32), src, stream)
 
     @classmethod
-    def _layout(cls, n: int, size: int, src: DeviceBuffer, stream) -> "DeviceBatch":
-        slot = (frame_bound(size) + 15) & ~15
-        frames = DeviceBuffer(n * slot + 64)
-        out = DeviceBuffer(n * ((size + 15) & ~15) + 64)
+    def _layout(cls, sizes: np.ndarray, src: DeviceBuffer, stream) -> "DeviceBatch":
+        n = len(sizes)
+        src_off = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            src_off[1:] = np.cumsum(sizes[:-1].astype(np.uint64))
+        uniq, inv = np.unique(sizes, return_inverse=True)
+        fslot = np.array([frame_bound(int(x)) for x in uniq], dtype=np.uint64)
+        slots = ((fslot + 15) & ~np.uint64(15))[inv]
+        frame_off = np.zeros(n, dtype=np.uint64)
+        if n > 1:
+            frame_off[1:] = np.cumsum(slots[:-1])
+        frames = DeviceBuffer(int(slots.sum()) + 64)
+        out = DeviceBuffer(src.nbytes)
         # meta: src_off u64 | len u32 | frame_off u64 | frame_len u32 | status i32 |
         #       out_off u64 | out_cap u32 | out_len u32 | dstatus i32
-        idx = np.arange(n, dtype=np.uint64)
         m = np.concatenate([
-            (idx * np.uint64(size)).view(np.uint8),
-            np.full(n, size, np.uint32).view(np.uint8),
-            (idx * np.uint64(slot)).view(np.uint8),
+            src_off.view(np.uint8),
+            sizes.view(np.uint8),
+            frame_off.view(np.uint8),
             np.zeros(n, np.uint32).view(np.uint8),
             np.zeros(n, np.int32).view(np.uint8),
-            (idx * np.uint64((size + 15) & ~15)).view(np.uint8),
-            np.full(n, size, np.uint32).view(np.uint8),
+            src_off.view(np.uint8),
+            sizes.view(np.uint8),
             np.zeros(n, np.uint32).view(np.uint8),
             np.zeros(n, np.int32).view(np.uint8),
         ])
@@ -346,7 +384,8 @@ class DeviceBatch:
         meta.upload(m, stream=stream.ptr if stream else None)
         if stream:
             stream.sync()
-        return cls(n=n, size=size, src=src, frames=frames, out=out, meta=meta, slot=slot)
+        return cls(n=n, size=int(sizes.max()) if n else 0, sizes=sizes, src_off=src_off, frame_off=frame_off,
+                   src=src, frames=frames, out=out, meta=meta, slot=int(slots.max()) if n else 16)
 
     # metadata views (device pointers)
     def _p(self, k: int) -> int:
@@ -375,6 +414,14 @@ class DeviceBatch:
 
     def out_lens(self) -> np.ndarray:
         return self.meta.download(4 * self.n, 40 * self.n).view(np.uint32)
+
+    def roundtrip_ok(self) -> bool:
+        """Every status 0, every decoded length right, every decoded byte equal."""
+        cst, dst = self.status()
+        if not ((cst == 0).all() and (dst == 0).all() and np.array_equal(self.out_lens(), self.sizes)):
+            return False
+        t = self.raw_bytes
+        return bool(np.array_equal(self.src.download(t), self.out.download(t)))
 
     def free(self) -> None:
         for b in (self.src, self.frames, self.out, self.meta):

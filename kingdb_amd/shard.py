@@ -70,13 +70,14 @@ def g1_first_piece(rank: int, values_per_rank: int, value_bytes: int) -> int:
     return rank * ((values_per_rank * value_bytes + 99) // 100)
 
 
-def max_over_ranks(seconds: float) -> float:
-    """Max elapsed time over all ranks (the bench's job time); identity when
-    torch.distributed is not initialised."""
+def max_over_ranks(seconds: float, op: str = "max") -> float:
+    """Max (or, with op="sum", the sum) of a scalar over all ranks -- the
+    bench's job time and its total bytes; identity when torch.distributed is
+    not initialised."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(seconds)
     t = torch.tensor([float(seconds)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
     return float(t.item())

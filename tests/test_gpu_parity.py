@@ -166,6 +166,29 @@ def test_device_batch_roundtrip_g1_long(gpu, orc):
     b.free()
 
 
+def test_device_batch_mixed_config4(gpu, orc):
+    """SURVEY §8d config 4 shape (100 B / 4 KiB / 64 KiB parts) in one batch,
+    plus the class edges (4096/4097, 8192/8193, 65546/65547): every size class
+    launch of compress and decompress, frames byte-identical to the oracle on a
+    sample, full round trip bit-exact."""
+    from kingdb_amd.lz4 import mixed_sizes
+    sizes = mixed_sizes(6000, mix=((100, 0.6), (4096, 0.25), (65536, 0.05), (4097, 0.02), (8192, 0.02),
+                                   (8193, 0.02), (65546, 0.01), (65547, 0.01), (13, 0.01), (12, 0.01)))
+    b = gpu.DeviceBatch.g1_long_sizes(sizes)
+    b.compress()
+    b.decompress()
+    assert b.roundtrip_ok()
+    src = b.src.download(b.raw_bytes)
+    flen = b.frame_lens()
+    frames = b.frames.download()
+    for i in list(range(0, b.n, 37)) + [b.n - 1]:
+        o, sz = int(b.src_off[i]), int(sizes[i])
+        exp = orc.frame(src[o:o + sz].tobytes())
+        fo = int(b.frame_off[i])
+        assert frames[fo:fo + int(flen[i])].tobytes() == exp, (i, sz)
+    b.free()
+
+
 def test_pack_frames(gpu):
     """kdb_lz4_pack_frames: ragged lengths, unaligned source and destination."""
     from kingdb_amd import lz4 as L
