@@ -58,6 +58,18 @@ SIGNATURES = {
     "kdb_lz4_decompress_frames_batch": (_i, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
     "kdb_lz4_pack_frames": (_i, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "kdb_lz4_gen_g1": (_i, [_vp, _u64, _u64, _u32, _vp]),
+    # include/kdb_put.h (the write path around the codec)
+    "kdb_put_scratch_bytes": (_u64, [_u32, _u32, _u64]),
+    "kdb_put_entries_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp, _u64,
+                                   _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "kdb_hstable_db_options": (_i, [_u64, _u32, _vp]),
+    "kdb_hstable_writer_create": (_i, [_u64, _u32, _c.POINTER(_vp)]),
+    "kdb_hstable_writer_append": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "kdb_hstable_writer_close": (_i, [_vp]),
+    "kdb_hstable_writer_file_count": (_i, [_vp, _c.POINTER(_u32)]),
+    "kdb_hstable_writer_file": (_i, [_vp, _u32, _c.POINTER(_u32), _c.POINTER(_vp), _c.POINTER(_u64)]),
+    "kdb_hstable_writer_save": (_i, [_vp, _c.c_char_p]),
+    "kdb_hstable_writer_destroy": (_i, [_vp]),
     # link-time aliases of the reference's lz4.h names
     "LZ4_compressBound": (_i, [_i]),
     "LZ4_compress_limitedOutput": (_i, [_c.c_char_p, _vp, _i, _i]),

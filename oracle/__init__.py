@@ -56,6 +56,22 @@ class Oracle:
         lib.orc_frame_uncompress.restype = ctypes.c_int
         lib.orc_g1_pieces.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u8p]
         lib.orc_g1_pieces.restype = None
+        c = ctypes
+        lib.orc_crc8.argtypes = [c.c_uint, _u8p, c.c_size_t]
+        lib.orc_crc8.restype = c.c_uint8
+        lib.orc_xxh64.argtypes = [_u8p, c.c_size_t, c.c_uint64]
+        lib.orc_xxh64.restype = c.c_uint64
+        lib.orc_murmur3_64.argtypes = [_u8p, c.c_size_t]
+        lib.orc_murmur3_64.restype = c.c_uint64
+        lib.orc_entry_header.argtypes = [c.c_uint32, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint64, c.c_uint64,
+                                         c.c_uint64, _u8p]
+        lib.orc_entry_header.restype = c.c_int
+        lib.orc_padding.argtypes = [c.c_uint64]
+        lib.orc_padding.restype = c.c_uint64
+        lib.orc_put_value.argtypes = [_u8p, c.c_uint32, _u8p, c.c_uint64, ctypes.POINTER(c.c_uint32), c.c_uint32,
+                                      _u8p, ctypes.POINTER(c.c_uint64), ctypes.POINTER(c.c_uint32),
+                                      ctypes.POINTER(c.c_uint64), ctypes.POINTER(c.c_uint32)]
+        lib.orc_put_value.restype = c.c_int
         self.lib = lib
 
     def compress_bound(self, n: int) -> int:
@@ -96,6 +112,49 @@ class Oracle:
         out = np.empty(npieces * 100, dtype=np.uint8)
         self.lib.orc_g1_pieces(seed, npieces, _ptr(out))
         return out
+
+    # ------------------------------------------------ write path
+    @staticmethod
+    def _buf(data: bytes) -> np.ndarray:
+        return np.frombuffer(data, dtype=np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
+
+    def crc8(self, data: bytes, crc: int = 0) -> int:
+        return self.lib.orc_crc8(crc, _ptr(self._buf(data)), len(data))
+
+    def xxh64(self, data: bytes, seed: int = 0) -> int:
+        return self.lib.orc_xxh64(_ptr(self._buf(data)), len(data), seed)
+
+    def murmur3_64(self, data: bytes) -> int:
+        return self.lib.orc_murmur3_64(_ptr(self._buf(data)), len(data))
+
+    def entry_header(self, crc: int, flags: int, size_key: int, size_value: int, svc: int, padding: int,
+                     hashed: int) -> bytes:
+        out = np.zeros(64, np.uint8)
+        n = self.lib.orc_entry_header(crc, flags, size_key, size_value, svc, padding, hashed, _ptr(out))
+        return out[:n].tobytes()
+
+    def padding(self, size_value: int) -> int:
+        return self.lib.orc_padding(size_value)
+
+    def put_value(self, key: bytes, value: bytes, chunks: list[int] | None = None) -> dict:
+        """Database::PutPart over `chunks` (default: one chunk) of one value:
+        {"parts": [(offset_chunk_compressed, chunk_final bytes)], "svc", "crc",
+        "stored": the value region (size_value + padding bytes)}; raises on IOError."""
+        chunks = [len(value)] if chunks is None else list(chunks)
+        assert sum(chunks) == len(value)
+        n = len(chunks)
+        cl = (ctypes.c_uint32 * max(n, 1))(*chunks)
+        po = (ctypes.c_uint64 * max(n, 1))()
+        pl = (ctypes.c_uint32 * max(n, 1))()
+        svc, crc = ctypes.c_uint64(0), ctypes.c_uint32(0)
+        stored = np.zeros(len(value) + self.padding(len(value)) + 64, np.uint8)
+        rc = self.lib.orc_put_value(_ptr(self._buf(key)), len(key), _ptr(self._buf(value)), len(value), cl, n,
+                                    _ptr(stored), po, pl, ctypes.byref(svc), ctypes.byref(crc))
+        if rc != 0:
+            raise RuntimeError("PutPartValidSize IOError")
+        parts = [(int(po[i]), stored[int(po[i]):int(po[i]) + int(pl[i])].tobytes()) for i in range(n)]
+        return {"parts": parts, "svc": svc.value, "crc": crc.value,
+                "stored": stored[: len(value) + self.padding(len(value))].tobytes()}
 
 
 class Reference:

@@ -1,0 +1,192 @@
+"""oracle.hstable -- TEST INFRASTRUCTURE ONLY.
+
+Pure-Python restatement of KingDB's embedded write path from the put stream
+to the HSTable file bytes, for one client thread:
+
+  Database::PutPart / PutPartValidSize   interface/database.cc:87-276
+      (frame policy, size_value_compressed, CRC32C -- via Oracle.put_value)
+  WriteBuffer::WritePart                 cache/write_buffer.cc:155-225 (is_large, Order)
+  HSTableManager::WriteOrdersAndFlushFile storage/hstable_manager.h:714-847
+      WriteFirstPartOrSmallOrder 628-712, WriteMiddleOrLastPart 514-626,
+      FlushCurrentFile 312-359, FlushOffsetArray/WriteOffsetArray 361-420,
+      OpenNewFile 260-290
+  EntryHeader / HSTableHeader / DatabaseOptionEncoder / HSTableFooter /
+      OffsetArrayRow encodings               storage/format.h
+
+It is the checker for kingdb_amd's GPU put path (csrc/put.hip) and its host
+HSTable writer (csrc/hstable.cc), and is itself pinned against the reference
+build (oracle/_ref/ref_db) by tests/golden/hstable_*.npz.
+
+Scope: one writer thread (the reference's per-thread policy state is then a
+single state), every flush of the write buffer treated as one batch (the
+`>` / `>=` size_block_ tests of WriteOrdersAndFlushFile and FlushCurrentFile
+then coincide except when a batch ends exactly on size_block_), no large
+entries (key + value > hstable size: their own file, not modelled).
+"""
+from __future__ import annotations
+
+import struct
+
+HEADER_SIZE = 8192                 # internal__hstable_header_size (util/options.h:43)
+MAGIC = 0x4D454F57                 # HSTableManager::get_magic_number (hstable_manager.h:1215)
+K_ENTRY_FULL, K_UNCOMPACTED, K_HAS_PADDING = 0x8, 0x2, 0x4   # format.h:34-42
+VERSION = (0, 9, 0, 0)             # util/version.h:10-13
+FORMAT = (1, 0)                    # format.h:28-29
+
+
+def varint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 128:
+        out.append((v & 127) | 128)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def db_options_bytes(orc, hstable_size: int, hash_type: int) -> bytes:
+    """DatabaseOptionEncoder::EncodeTo (format.h:324-340); also the db_options file."""
+    body = struct.pack("<IIIIIIQIII", *VERSION, *FORMAT, hstable_size, hash_type, 1, 1)
+    return struct.pack("<I", orc.crc32c(body)) + body
+
+
+def hstable_header_block(orc, timestamp: int, hstable_size: int, hash_type: int, filetype: int = 1) -> bytes:
+    """HSTableHeader::EncodeTo + options (format.h:415-425) padded to HEADER_SIZE."""
+    body = struct.pack("<IIIQ", *FORMAT, filetype, timestamp)
+    hdr = struct.pack("<I", orc.crc32c(body)) + body + db_options_bytes(orc, hstable_size, hash_type)
+    return hdr + bytes(HEADER_SIZE - len(hdr))
+
+
+class Writer:
+    """The reference's HSTable output for a sequential put stream."""
+
+    def __init__(self, orc, hstable_size: int = 32 << 20, hash_type: int = 1):
+        self.orc = orc
+        self.size_block = hstable_size
+        self.hash_type = hash_type
+        self.files: dict[int, bytearray] = {}
+        self.fileid = 0            # sequence file id (ids start at 1)
+        self.timestamp = 0
+        self.cur = None            # current file id or None
+        self.offset_end = 0
+        self.offarray: dict[int, list] = {}
+        self.padding_flag: dict[int, bool] = {}
+        self.in_progress: dict[int, int] = {}
+        self.location: dict[bytes, tuple[int, int]] = {}
+        self.headersize: dict[bytes, int] = {}
+        self.log: list[list] = []   # per first-part order: [file id, offset, entry bytes, hash, kind]
+
+    # ---- file management
+    def hash(self, key: bytes) -> int:
+        return self.orc.xxh64(key) if self.hash_type == 1 else self.orc.murmur3_64(key)
+
+    def _open(self) -> None:
+        self.fileid += 1
+        self.timestamp += 1
+        self.cur = self.fileid
+        self.files[self.cur] = bytearray(hstable_header_block(self.orc, self.timestamp, self.size_block,
+                                                              self.hash_type))
+        self.offset_end = HEADER_SIZE
+        self.offarray[self.cur] = []
+        self.padding_flag[self.cur] = False
+        self.in_progress[self.cur] = 0
+
+    def _write_offarray(self, fid: int) -> None:
+        f = self.files[fid]
+        rows = b"".join(varint(h) + varint(o) for h, o in self.offarray[fid])
+        footer = struct.pack("<IIQQQ", 1, 1 if self.padding_flag[fid] else 0, len(f), len(self.offarray[fid]), MAGIC)
+        body = rows + footer
+        f += body + struct.pack("<I", self.orc.crc32c(body))
+
+    def _close(self) -> None:
+        if self.cur is None:
+            return
+        if self.in_progress[self.cur] == 0:
+            del self.files[self.cur][self.offset_end:]
+            self._write_offarray(self.cur)
+        self.cur = None
+
+    def _flush(self, force: int = 0, padding: int = 0) -> None:
+        if self.cur is None:
+            return
+        if padding:
+            self.offset_end += padding
+            f = self.files[self.cur]
+            if len(f) < self.offset_end:
+                f += bytes(self.offset_end - len(f))
+        if self.offset_end >= self.size_block or (force and self.offset_end > HEADER_SIZE):
+            self._close()
+
+    # ---- entries
+    def _header(self, crc, flags, klen, size_value, svc, padding, hashed) -> bytes:
+        return self.orc.entry_header(crc, flags, klen, size_value, svc, padding, hashed)
+
+    def _order(self, key: bytes, chunk: bytes, occ: int, size_value: int, svc: int, crc: int) -> None:
+        if self.offset_end > self.size_block:
+            self._flush(force=1)
+        if self.cur is None:
+            self._open()
+        hashed = self.hash(key)
+        first = occ == 0
+        last = (svc == 0 and len(chunk) + occ == size_value) or (svc != 0 and len(chunk) + occ == svc)
+        if len(key) + size_value > self.size_block:
+            raise NotImplementedError("large entries (own HSTable) are not modelled")
+        if not first:
+            fid, off = self.location.get(key, (0, 0))
+            if fid == 0 or (fid != self.cur and self.in_progress[fid] == 0):
+                return
+            f = self.files[fid]
+            hs = self.headersize[key]
+            p = off + hs + len(key) + occ
+            f[p:p + len(chunk)] = chunk
+            if last:
+                flags = K_ENTRY_FULL | (K_UNCOMPACTED | K_HAS_PADDING if svc > 0 else 0)
+                hdr = self._header(crc, flags, len(key), size_value, svc, self.orc.padding(size_value), hashed)
+                f[off:off + len(hdr)] = hdr
+                self.in_progress[fid] -= 1
+                for rec in reversed(self.log):
+                    if rec[0] == fid and rec[1] == off:
+                        rec[4] = 1
+                        break
+                if fid != self.cur and self.in_progress[fid] == 0:
+                    self._write_offarray(fid)
+                del self.location[key]
+                self.headersize.pop(key, None)
+            return
+        selfc = last
+        flags = K_ENTRY_FULL | (0 if selfc else K_UNCOMPACTED | K_HAS_PADDING)
+        pad = 0 if selfc else self.orc.padding(size_value)
+        hdr = self._header(crc, flags, len(key), size_value, svc, pad, hashed)
+        f = self.files[self.cur]
+        off = self.offset_end
+        entry = hdr + key + chunk
+        del f[off:]
+        f += entry
+        self.offarray[self.cur].append((hashed, off))
+        self.offset_end += len(entry)
+        self.log.append([self.cur, off, len(entry) if selfc else len(hdr) + len(key) + size_value + pad, hashed,
+                         0 if selfc else 2])
+        if not selfc:
+            self.location[key] = (self.cur, off)
+            self.headersize[key] = len(hdr)
+            self.padding_flag[self.cur] = True
+            self.in_progress[self.cur] += 1
+            self._flush(0, size_value + pad - len(chunk))
+
+    def put(self, key: bytes, value: bytes, chunks: list[int] | None = None) -> None:
+        """Database::PutPart for each chunk of one value, then the orders it makes."""
+        pv = self.orc.put_value(key, value, chunks)
+        n = len(pv["parts"])
+        for i, (occ, final) in enumerate(pv["parts"]):
+            lastcall = i == n - 1
+            self._order(key, final, occ, len(value), pv["svc"] if lastcall else 0, pv["crc"] if lastcall else 0)
+
+    def dense(self):
+        """The per-value view the GPU put path produces (kdb_put_entries_batch):
+        (entry bytes, key hash, kind) per first-part order, in order; call after close()."""
+        return [(bytes(self.files[fid][off:off + ln]), h, k) for fid, off, ln, h, k in self.log]
+
+    def close(self) -> dict[str, bytes]:
+        """End of the batch and Database::Close: {"00000001": bytes, ...}."""
+        self._flush(0, 0)
+        self._close()
+        return {"%08x" % fid: bytes(b) for fid, b in sorted(self.files.items())}

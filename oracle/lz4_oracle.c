@@ -23,6 +23,7 @@
  */
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 /* ---- constants: lz4.cc:222-246, lz4.h:60,102-103 ---------------------- */
@@ -333,6 +334,193 @@ int orc_frame_uncompress(const uint8_t* frame, uint8_t* out, uint64_t* out_n, ui
     *out_n = raw;
     *frame_n = (uint64_t)raw + 8;
   }
+  return 0;
+}
+
+/* ---- Write path: CRC-8, varints, key hashes, EntryHeader,
+ *      Database::PutPartValidSize's frame policy ---------------------------- */
+
+/* crc32c::crc8 (crc32c.cc:439-475): reflected CRC-8, table for polynomial 0xB2
+ * (reflected), pre/post xor 0xff; crc8(c, p, 0) returns c unchanged. */
+static uint8_t crc8_table[256];
+static int crc8_done = 0;
+uint8_t orc_crc8(unsigned crc, const uint8_t* p, size_t n) {
+  if (!crc8_done) {
+    for (unsigned i = 0; i < 256; i++) {
+      unsigned c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xB2u : c >> 1;
+      crc8_table[i] = (uint8_t)c;
+    }
+    crc8_done = 1;
+  }
+  if (n == 0) return (uint8_t)crc;
+  crc ^= 0xffu;
+  for (size_t i = 0; i < n; i++) crc = crc8_table[(crc ^ p[i]) & 0xffu];
+  return (uint8_t)(crc ^ 0xffu);
+}
+
+/* EncodeVarint32/64 (algorithm/coding.cc, LevelDB format): 7 bits per byte, LE. */
+static uint8_t* put_varint64(uint8_t* p, uint64_t v) {
+  while (v >= 128) { *p++ = (uint8_t)(v | 128); v >>= 7; }
+  *p++ = (uint8_t)v;
+  return p;
+}
+static uint8_t* put_fixed32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i)); return p + 4; }
+static uint8_t* put_fixed64(uint8_t* p, uint64_t v) { for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i)); return p + 8; }
+static inline uint64_t rd64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+/* XXH64(data, len, 0) (algorithm/xxhash.cc:427, hash.cc:20-23). */
+#define XP1 11400714785074694791ULL
+#define XP2 14029467366897019727ULL
+#define XP3 1609587929392839161ULL
+#define XP4 9650029242287828579ULL
+#define XP5 2870177450012600261ULL
+static inline uint64_t xround(uint64_t acc, uint64_t in) { acc += in * XP2; acc = rotl64(acc, 31); return acc * XP1; }
+static inline uint64_t xmerge(uint64_t acc, uint64_t v) { acc ^= xround(0, v); return acc * XP1 + XP4; }
+uint64_t orc_xxh64(const uint8_t* p, size_t len, uint64_t seed) {
+  const uint8_t* end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + XP1 + XP2, v2 = seed + XP2, v3 = seed, v4 = seed - XP1;
+    const uint8_t* lim = end - 32;
+    do {
+      v1 = xround(v1, rd64(p)); v2 = xround(v2, rd64(p + 8));
+      v3 = xround(v3, rd64(p + 16)); v4 = xround(v4, rd64(p + 24));
+      p += 32;
+    } while (p <= lim);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h = xmerge(h, v1); h = xmerge(h, v2); h = xmerge(h, v3); h = xmerge(h, v4);
+  } else {
+    h = seed + XP5;
+  }
+  h += (uint64_t)len;
+  while (p + 8 <= end) { h ^= xround(0, rd64(p)); h = rotl64(h, 27) * XP1 + XP4; p += 8; }
+  if (p + 4 <= end) { h ^= (uint64_t)rd32(p) * XP1; h = rotl64(h, 23) * XP2 + XP3; p += 4; }
+  while (p < end) { h ^= (uint64_t)(*p) * XP5; h = rotl64(h, 11) * XP1; p++; }
+  h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32;
+  return h;
+}
+
+/* MurmurHash3_x64_128(data, len, 0) first 8 bytes (murmurhash3.cc:255-330, hash.cc:9-17). */
+static inline uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL; k ^= k >> 33;
+  return k;
+}
+uint64_t orc_murmur3_64(const uint8_t* data, size_t len) {
+  const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+  uint64_t h1 = 0, h2 = 0;
+  const size_t nb = len / 16;
+  for (size_t i = 0; i < nb; i++) {
+    uint64_t k1 = rd64(data + 16 * i), k2 = rd64(data + 16 * i + 8);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  }
+  const uint8_t* t = data + nb * 16;
+  uint64_t k1 = 0, k2 = 0;
+  size_t r = len & 15;
+  for (size_t i = r; i > 8; i--) k2 ^= (uint64_t)t[i - 1] << (8 * (i - 9));
+  if (r > 8) { k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2; }
+  for (size_t i = (r < 8 ? r : 8); i > 0; i--) k1 ^= (uint64_t)t[i - 1] << (8 * (i - 1));
+  if (r > 0) { k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1; }
+  h1 ^= (uint64_t)len; h2 ^= (uint64_t)len;
+  h1 += h2; h2 += h1;
+  h1 = fmix64(h1); h2 = fmix64(h2);
+  h1 += h2;
+  return h1;
+}
+
+/* EntryHeader::EncodeTo with compression on (storage/format.h:224-255): crc8
+ * byte, fixed32 checksum_content, varint flags / size_key / size_value, fixed64
+ * size_value_compressed, varint size_padding, fixed64 hash.  Returns its size. */
+int orc_entry_header(uint32_t checksum, uint32_t flags, uint64_t size_key, uint64_t size_value,
+                     uint64_t size_value_compressed, uint64_t size_padding, uint64_t hash, uint8_t* out) {
+  uint8_t* p = put_fixed32(out + 1, checksum);
+  p = put_varint64(p, flags);
+  p = put_varint64(p, size_key);
+  p = put_varint64(p, size_value);
+  p = put_fixed64(p, size_value_compressed);
+  p = put_varint64(p, size_padding);
+  p = put_fixed64(p, hash);
+  out[0] = orc_crc8(0, out + 1, (size_t)(p - out) - 1);
+  return (int)(p - out);
+}
+
+/* EntryHeader::CalculatePaddingSize (format.h:63-71). */
+uint64_t orc_padding(uint64_t size_value) { return (size_value / 65536u + 1u) * 8u; }
+
+/*
+ * Database::PutPartValidSize (interface/database.cc:128-276) for every chunk of
+ * one value, sent in order by one thread (offset = bytes already sent), with
+ * LZ4 compression on.  Per chunk i: part_off[i] = offset_chunk_compressed,
+ * part_len[i] = bytes of chunk_final, written to stored + part_off[i] (stored
+ * holds size_value + padding bytes).  Also *svc = size_value_compressed (set on
+ * the last chunk, 0 when the value is empty) and *crc = CRC32C(key || every
+ * chunk_final), as handed to WriteBuffer::PutPart.  Returns 0, or -1 where the
+ * reference returns an IOError (compressor failure, or the write-outside-the-
+ * allocated-memory check at database.cc:263-267).
+ */
+int orc_put_value(const uint8_t* key, uint32_t klen, const uint8_t* value, uint64_t size_value,
+                  const uint32_t* chunk_len, uint32_t nchunks, uint8_t* stored, uint64_t* part_off,
+                  uint32_t* part_len, uint64_t* svc, uint32_t* crc) {
+  int enabled = 1;
+  uint64_t ts_offset = 0, comp_total = 0, off = 0;
+  const uint64_t pad = orc_padding(size_value);
+  uint32_t c32 = 0;
+  *svc = 0;
+  uint8_t* fr = (uint8_t*)malloc(8 + 2 * (size_t)size_value + 64);
+  for (uint32_t i = 0; i < nchunks; i++) {
+    const uint64_t csz = chunk_len[i];
+    const uint8_t* chunk = value + off;
+    const int first = off == 0, last = csz + off == size_value;
+    const int do_comp = csz != 0;                                     /* :155-158 */
+    uint64_t occ = off;
+    if (first) { enabled = 1; ts_offset = 0; }                        /* :160-163 */
+    if (!enabled) { occ = ts_offset; ts_offset = occ + csz; }         /* :165-172 */
+    const uint8_t* fin = chunk;
+    uint64_t fsz = csz;
+    int hdr_zero = 0;
+    if (do_comp && enabled) {
+      if (first) comp_total = 0;                                      /* :178-180 */
+      occ = comp_total;                                               /* :183 */
+      int64_t F = orc_frame_compress(chunk, csz, fr);                 /* :186-189 */
+      if (F < 0) { free(fr); return -1; }
+      comp_total += (uint64_t)F;
+      const uint64_t size_remaining = size_value - off;               /* :197-199 */
+      const uint64_t space_left = size_value + pad - occ;
+      if (size_remaining - csz + 8u > space_left - (uint64_t)F) {     /* :200-209 */
+        comp_total -= (uint64_t)F;
+        fsz = csz + 8u;
+        enabled = 0;
+        ts_offset = comp_total + fsz;
+        hdr_zero = 1;
+      } else {
+        fin = fr;
+        fsz = (uint64_t)F;
+      }
+    }
+    if (do_comp && last) {                                            /* :237-248 */
+      if (enabled) *svc = comp_total;
+      else if (first) *svc = ts_offset;
+      else *svc = occ + csz;
+    }
+    if (occ + fsz > size_value + (do_comp ? pad : 0)) { free(fr); return -1; }   /* :261-267 */
+    if (first) c32 = orc_crc32c_extend(0, key, klen);                 /* :251-256 */
+    if (hdr_zero) {
+      memset(stored + occ, 0, 8);
+      memcpy(stored + occ + 8, chunk, csz);
+    } else if (fsz) {
+      memcpy(stored + occ, fin, fsz);
+    }
+    c32 = orc_crc32c_extend(c32, stored + occ, fsz);
+    part_off[i] = occ;
+    part_len[i] = (uint32_t)fsz;
+    off += csz;
+  }
+  free(fr);
+  *crc = c32;
   return 0;
 }
 

@@ -1,0 +1,81 @@
+// oracle/ref_db.cc -- TEST INFRASTRUCTURE ONLY (compiled into oracle/_ref/ by
+// `make -C oracle ref`, linked against the REFERENCE's own objects compiled in
+// place from /root/reference; no reference source is copied here).
+//
+// Drives the real KingDB write path (Database::PutPart -> WriteBuffer ->
+// HSTableManager, interface/database.cc:87-276, storage/hstable_manager.h:628-847)
+// over a put stream read from a file, then closes the database so every
+// HSTable is flushed with its offset array.  tests/golden/make_golden.py runs
+// it to pin the write-path restatement (oracle/lz4_oracle.c orc_put_*) and the
+// GPU put kernels against the bytes the reference itself writes.
+//
+//   ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash]]]   (hash: 0 murmur3, 1 xxhash)
+//
+// stream.bin: records of
+//   u32 key_len, key bytes, u64 size_value, u32 nchunks,
+//   nchunks x (u32 chunk_len, chunk bytes)
+// and each chunk is handed to Database::PutPart(key, chunk, offset, size_value)
+// in order (offset = bytes of the value already sent), like a client
+// streaming a value in parts (network/server.cc:258).
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "interface/database.h"
+#include "util/byte_array.h"
+#include "util/status.h"
+
+static bool rd(FILE* f, void* p, size_t n) { return n == 0 || fread(p, 1, n, f) == n; }
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash]]]\n");
+    return 2;
+  }
+  kdb::Logger::set_current_level("emerg");
+  kdb::DatabaseOptions options;
+  options.compression = kdb::kLZ4Compression;
+  if (argc > 3) options.storage__maximum_part_size = strtoull(argv[3], nullptr, 0);
+  if (argc > 4) options.storage__hstable_size = strtoull(argv[4], nullptr, 0);
+  if (argc > 5) options.hash = strtoul(argv[5], nullptr, 0) ? kdb::kxxHash_64 : kdb::kMurmurHash3_64;
+  kdb::Database db(options, argv[1]);
+  kdb::Status s = db.Open();
+  if (!s.IsOK()) {
+    fprintf(stderr, "open: %s\n", s.ToString().c_str());
+    return 1;
+  }
+  FILE* f = fopen(argv[2], "rb");
+  if (!f) return 1;
+  kdb::WriteOptions wo;
+  uint64_t puts = 0;
+  for (;;) {
+    uint32_t klen;
+    if (fread(&klen, 4, 1, f) != 1) break;
+    std::string key(klen, '\0');
+    uint64_t vsize;
+    uint32_t nchunks;
+    if (!rd(f, &key[0], klen) || !rd(f, &vsize, 8) || !rd(f, &nchunks, 4)) return 1;
+    uint64_t off = 0;
+    for (uint32_t c = 0; c < nchunks; c++) {
+      uint32_t clen;
+      if (!rd(f, &clen, 4)) return 1;
+      std::vector<char> buf(clen);
+      if (!rd(f, buf.data(), clen)) return 1;
+      kdb::ByteArray k = kdb::NewDeepCopyByteArray(key.data(), key.size());
+      kdb::ByteArray v = kdb::NewDeepCopyByteArray(buf.data(), clen);
+      s = db.PutPart(wo, k, v, off, vsize);
+      if (!s.IsOK()) {
+        fprintf(stderr, "put %llu: %s\n", (unsigned long long)puts, s.ToString().c_str());
+        return 1;
+      }
+      off += clen;
+    }
+    puts++;
+  }
+  fclose(f);
+  db.Close();
+  printf("%llu puts\n", (unsigned long long)puts);
+  return 0;
+}

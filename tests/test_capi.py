@@ -11,16 +11,19 @@ from conftest import ROOT
 
 
 def header_symbols():
-    text = open(os.path.join(ROOT, "include", "kdb_lz4.h")).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(kdb_lz4_\w+)\s*\(", text)))
+    syms = set()
+    for h in ("kdb_lz4.h", "kdb_put.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        syms |= set(re.findall(r"\b(kdb_(?:lz4|put|hstable)_\w+)\s*\(", text))
+    return sorted(syms)
 
 
 def test_library_exports_every_header_symbol():
     from kingdb_amd import _lib
     lib = _lib.load()
     syms = header_symbols()
-    assert len(syms) >= 25
+    assert len(syms) >= 35
     for s in syms:
         assert hasattr(lib, s), s
         assert s in _lib.SIGNATURES, f"{s} missing from the ctypes signature table"
