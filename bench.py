@@ -43,9 +43,11 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--values", type=int, default=1 << 20, help="values per GPU")
     p.add_argument("--size", type=int, default=4096, help="bytes per value")
-    p.add_argument("--workload", choices=("uniform", "mixed"), default="uniform",
+    p.add_argument("--workload", choices=("uniform", "mixed", "put"), default="uniform",
                    help="uniform: --values x --size (configs[2], the headline); mixed: configs[3], "
-                        "--values per GPU of 90%% 100 B / 9%% 4 KiB / 1%% 64 KiB parts, byte-balanced shards")
+                        "--values per GPU of 90%% 100 B / 9%% 4 KiB / 1%% 64 KiB parts, byte-balanced shards; "
+                        "put: configs[4], --values puts per GPU of 16 B keys / 100 B values from pinned host "
+                        "memory to HSTable file bytes in host memory")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU leg")
     p.add_argument("--no-verify", action="store_true")
@@ -150,6 +152,114 @@ def host_inclusive(batch, n: int, size: int, args) -> dict:
     return res
 
 
+def ref_write_path(keys: np.ndarray, vals: np.ndarray) -> dict | None:
+    """configs[4] CPU path: the reference's own Database::PutPart -> WriteBuffer ->
+    HSTableManager (oracle/_ref/ref_db, built from /root/reference) on the same
+    puts, writing its HSTables to a scratch directory; None where not built."""
+    import shutil
+    import struct
+    import subprocess
+    import tempfile
+    import oracle  # checker / baseline only
+    exe = os.path.join(os.path.dirname(oracle.REF_SO), "ref_db")
+    if not os.path.exists(exe):
+        return None
+    n, ks = keys.shape
+    vs = vals.shape[1]
+    rec = np.zeros((n, 4 + ks + 8 + 4 + 4 + vs), np.uint8)
+    rec[:, 0:4] = np.frombuffer(struct.pack("<I", ks), np.uint8)
+    rec[:, 4:4 + ks] = keys
+    rec[:, 4 + ks:12 + ks] = np.frombuffer(struct.pack("<Q", vs), np.uint8)
+    rec[:, 12 + ks:16 + ks] = np.frombuffer(struct.pack("<I", 1), np.uint8)
+    rec[:, 16 + ks:20 + ks] = np.frombuffer(struct.pack("<I", vs), np.uint8)
+    rec[:, 20 + ks:] = vals
+    d = tempfile.mkdtemp(prefix="kdbref")
+    try:
+        rec.tofile(os.path.join(d, "s.bin"))
+        r = subprocess.run([exe, os.path.join(d, "db"), os.path.join(d, "s.bin")], check=True, capture_output=True,
+                           text=True, timeout=300)
+        f = r.stdout.split()
+        t_put, t_all = float(f[2]), float(f[5])
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return {"value": round(n / t_put, 1), "unit": "puts/s", "cores": 1, "kind": "reference",
+            "sample": f"{n} puts ({ks} B keys, {vs} B G1 values), the GPU batch's own, one client thread "
+                      f"(KingDB's write buffer and storage threads behind it), HSTables on local disk; "
+                      f"CPU: {cpu_model()}",
+            "with_close_puts_per_s": round(n / t_all, 1), "seconds_put": round(t_put, 4),
+            "seconds_with_close": round(t_all, 4),
+            "source": "interface/database.cc PutPart -> cache/write_buffer.cc -> storage/hstable_manager.h, "
+                      "compiled from the reference (oracle/_ref/ref_db)"}
+
+
+def bench_put(args, world: int, rank: int, local: int, barrier, sync_all) -> None:
+    """configs[4]: the write path, host memory to HSTable bytes, PCIe included."""
+    from kingdb_amd.lz4 import DeviceBuffer
+    from kingdb_amd.putpipe import PutPipeline
+    from kingdb_amd.shard import max_over_ranks
+    n, ks, vs = args.values, 16, 100
+    pp = PutPipeline(n, ks, vs, chunk=args.hi_chunk, nstreams=args.hi_streams)
+    base = rank * n                                   # this rank's slice of one global put sequence
+    keys = np.frombuffer(b"".join(b"%016d" % (base + i) for i in range(n)), np.uint8).reshape(n, ks)
+    pp.h_keys.np[:] = keys.reshape(-1)
+    g = DeviceBuffer(n * vs + 64)
+    from kingdb_amd import _lib
+    from kingdb_amd import lz4 as L
+    _lib.check(L.lib().kdb_lz4_gen_g1(g.ptr, base, n, 301, None), "gen_g1")   # 100-byte G1 pieces = values
+    pp.h_vals.np[:] = g.download(n * vs)
+    g.free()
+    for _ in range(args.warmup):
+        pp.run()
+    times = []
+    barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        times.append(pp.run())
+    sync_all()
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    # what was timed: every put accepted, entries framed in order (spot-check the
+    # first entries' keys and sizes; byte parity is tests/test_write_path.py's job)
+    files = pp.writer.files()
+    first = files[min(files)]
+    pos, ok = 8192, True
+    for i in range(min(n, 1000)):
+        h = first[pos:pos + 64]
+        # EntryHeader: crc8, fixed32, varint flags, varint size_key, varint size_value, fixed64 svc, varint pad, fixed64
+        ok &= h[5] == 8 and h[6] == ks and h[7] == vs
+        svc = int.from_bytes(h[8:16], "little")
+        ok &= first[pos + 25:pos + 25 + ks] == keys[i].tobytes()
+        pos += 25 + ks + (svc if svc else vs)
+    if not ok:
+        raise SystemExit("bench: write-path output malformed -- refusing to report a number")
+    total = max_over_ranks(float(n), op="sum") * args.steps
+    file_bytes = pp.writer.file_bytes()
+    line = {
+        "metric": "KingDB write path puts/s (16 B keys / 100 B values, pinned host memory -> HSTable bytes, PCIe "
+                  "included)",
+        "value": round(total / elapsed, 1), "unit": "puts/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: %016d keys, 100-byte G1 values (db_bench CompressibleString 0.5)",
+        "config": {"workload": f"configs[4]: {n} puts per GPU through Database::PutPart semantics (frame policy, "
+                               f"LZ4, CRC32C, xxHash-64, EntryHeader) into HSTable files, one writer per GPU",
+                   "puts_per_gpu": n, "key_bytes": ks, "value_bytes": vs, "chunk": pp.chunk,
+                   "streams": len(pp.streams), "parallelism": f"dp{world} (independent shards, no collective)"},
+        "mb_per_s_in": round(total * (ks + vs) / elapsed / 1e6, 1),
+        "mb_per_s_out": round(file_bytes * max_over_ranks(1.0, op="sum") * args.steps / elapsed / 1e6, 1),
+        "hstable_bytes_per_gpu": file_bytes, "files_per_gpu": len(files),
+        "step_seconds": [round(t, 4) for t in times],
+        "last_step_host_seconds": {k: round(v, 4) for k, v in pp.stats.items()},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = ref_write_path(keys, pp.h_vals.np.reshape(n, vs))
+    pp.free()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def main() -> None:
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -182,6 +292,12 @@ def main() -> None:
     def barrier():
         if world > 1:
             dist.barrier()
+
+    if args.workload == "put":
+        bench_put(args, world, rank, local, barrier, sync_all)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     n, size = args.values, args.size
     stream = K.Stream()

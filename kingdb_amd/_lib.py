@@ -69,6 +69,7 @@ SIGNATURES = {
     "kdb_hstable_writer_file_count": (_i, [_vp, _c.POINTER(_u32)]),
     "kdb_hstable_writer_file": (_i, [_vp, _u32, _c.POINTER(_u32), _c.POINTER(_vp), _c.POINTER(_u64)]),
     "kdb_hstable_writer_save": (_i, [_vp, _c.c_char_p]),
+    "kdb_hstable_writer_reset": (_i, [_vp]),
     "kdb_hstable_writer_destroy": (_i, [_vp]),
     # link-time aliases of the reference's lz4.h names
     "LZ4_compressBound": (_i, [_i]),

@@ -90,11 +90,13 @@ class PutBatch:
 
     def run_device(self, stream, n: int, nparts: int, max_chunk: int, raw: int, hash_type: int) -> None:
         """Launches kdb_put_entries_batch on what is already resident."""
-        v = self.vmeta.ptr
+        if n > self.n or nparts > self.nparts or raw > self.raw:
+            raise ValueError("batch larger than the buffers")
+        v, c = self.vmeta.ptr, self.n     # metadata laid out for the capacity (a short batch uses a prefix)
         o = self._optr(n)
         _lib.check(lib().kdb_put_entries_batch(
-            stream.ptr if stream else None, self.keys.ptr, v, v + 8 * n, self.values.ptr, v + 12 * n, v + 20 * n,
-            v + 28 * n, self.chunks.ptr, nparts, max_chunk, n, hash_type, self.scratch.ptr, self.scratch_bytes, raw,
+            stream.ptr if stream else None, self.keys.ptr, v, v + 8 * c, self.values.ptr, v + 12 * c, v + 20 * c,
+            v + 28 * c, self.chunks.ptr, nparts, max_chunk, n, hash_type, self.scratch.ptr, self.scratch_bytes, raw,
             self.entries.ptr, o["entry_off"], o["entry_len"], o["total"], o["hashed"], o["crc"], o["kind"],
             o["status"]), "kdb_put_entries_batch")
 
@@ -179,6 +181,10 @@ class HSTableWriter:
 
     def close(self) -> None:
         _lib.check(lib().kdb_hstable_writer_close(self.h), "hstable_writer_close")
+
+    def reset(self) -> None:
+        """A fresh directory; the file buffers' memory is kept for reuse."""
+        _lib.check(lib().kdb_hstable_writer_reset(self.h), "hstable_writer_reset")
 
     def files(self) -> dict[str, bytes]:
         c = ctypes.c_uint32(0)
