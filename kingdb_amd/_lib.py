@@ -62,6 +62,9 @@ SIGNATURES = {
     "kdb_put_scratch_bytes": (_u64, [_u32, _u32, _u64]),
     "kdb_put_entries_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp, _u64,
                                    _u64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "kdb_get_scratch_bytes": (_u64, [_u32, _u64]),
+    "kdb_get_values_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _i, _vp, _vp, _u64, _u32, _u32, _vp,
+                                  _u64, _vp, _vp]),
     "kdb_hstable_db_options": (_i, [_u64, _u32, _vp]),
     "kdb_hstable_writer_create": (_i, [_u64, _u32, _c.POINTER(_vp)]),
     "kdb_hstable_writer_append": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <mutex>
 #include <unordered_map>
@@ -57,6 +59,13 @@ uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
+  static const int cap = [] {
+    const char* e = getenv("KDB_LZ4_PER_CU");     // diagnostic: cap workgroups per CU
+    return e && *e ? atoi(e) : 0;
+  }();
+  if (cap > 0 && per_cu > cap) per_cu = cap;
+  static const bool dbg = getenv("KDB_LZ4_DEBUG") != nullptr;
+  if (dbg) fprintf(stderr, "persistent_grid: lds=%zu per_cu=%d cus=%d\n", lds, per_cu, cus);
   uint64_t slots = (uint64_t)per_cu * (uint64_t)cus;
 #ifdef KDB_ABL_GRID_MULT
   slots *= KDB_ABL_GRID_MULT;   // diagnostic: oversubscribe the persistent grid

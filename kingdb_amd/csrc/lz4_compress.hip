@@ -74,6 +74,30 @@ struct Table {
   }
 };
 
+// byU16 table for values <= 4 KiB, whose positions fit 12 bits: two planes,
+// the low bytes (8192 x u8) and the high nibbles (4096 x u8, two per byte),
+// 12 KiB instead of 16 -- 16 KiB of LDS per value with its bytes, so 10
+// values per CU instead of 8 (the parse is latency-bound: occupancy is speed).
+// Cleared per value (12 x 16 B stores per lane).  The nibble half is written
+// with LDS and/or atomics: two lanes of one chunk may own the two nibbles of
+// one byte (hashes 2k, 2k+1).
+struct Table12 {
+  uint8_t* lo;
+  uint8_t* hi;
+  __device__ __forceinline__ uint32_t get(uint32_t h) const {
+    const uint32_t a = lo[h], b = hi[h >> 1];
+    return a | (((b >> ((h & 1u) << 2)) & 15u) << 8);
+  }
+  __device__ __forceinline__ void put(uint32_t h, uint32_t p) const {
+    lo[h] = (uint8_t)p;
+    uint32_t* w = reinterpret_cast<uint32_t*>(hi + ((h >> 1) & ~3u));
+    const uint32_t sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
+    __hip_atomic_fetch_and(w, ~(15u << sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(w, ((p >> 8) & 15u) << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+constexpr uint32_t kTable12Bytes = 8192u + 4096u;
+
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
 struct Table32 {
   uint32_t* t;
@@ -207,7 +231,7 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
           if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
           pe_total = 0;
         }
-        if (kb == 0 && t0) tab.put(hashp<kWide>(sm2), s - 3u);
+        if (kb == 0 && t0 && lane == 0) tab.put(hashp<kWide>(sm2), s - 3u);
         const uint32_t h = hashp<kWide>(seq);
         const uint32_t told = tab.get(h);
         const uint64_t vm = ballot(valid);
@@ -406,12 +430,16 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
-  uint8_t* s_in = smem + kTableBytes;    // value bytes [0, S), 16B-aligned
+  constexpr uint32_t kTabBytes = kSmall ? kTable12Bytes : kTableBytes;
+  uint8_t* s_in = smem + kTabBytes;      // value bytes [0, S), 16B-aligned
   const uint4 z4 = make_uint4(0, 0, 0, 0);
 
-  Table<kSmall> tab{tab16, 1u};
+  using Tab = typename std::conditional<kSmall, Table12, Table<false>>::type;
+  Tab tab;
+  if constexpr (kSmall) tab = Table12{smem, smem + 8192u};
+  else tab = Table<false>{tab16, 0u};
   if (kSmall) {
-    for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
+    for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(smem)[i] = z4;
   }
   // register prefetch (kSmall): the next value's realigned 16-byte chunks
   uint4 pa[kPrefetch], pb[kPrefetch];
@@ -485,13 +513,11 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
         if (lane == 0) { ret[v] = 0; frame_len[v] = flen; }
       }
     }
-    if (kSmall) {
-      if (++tab.gen == 16u) {                    // tags exhausted: clear (lz4.cc:669)
-        tab.gen = 1u;
+    if (kSmall) {                                // a zeroed table per value (lz4.cc:669)
 #ifndef KDB_ABL_NO_ZERO
-        for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
+#pragma unroll
+      for (uint32_t k = 0; k < kTabBytes / 1024u; ++k) reinterpret_cast<uint4*>(smem)[lane + 64u * k] = z4;
 #endif
-      }
     }
     __syncthreads();
     v = vn;
@@ -500,8 +526,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
-  const uint32_t m = max_len <= kSmallMax ? kSmallMax : max_len;
-  return kTableBytes + (((size_t)m + 15u) & ~(size_t)15u);
+  if (max_len <= kSmallMax) return kTable12Bytes + kSmallMax;   // 16 KiB: 10 per CU
+  return kTableBytes + (((size_t)max_len + 15u) & ~(size_t)15u);
 }
 
 // ---------------------------------------------------------------------------

@@ -38,6 +38,7 @@
 #include <cstdint>
 
 #include "../../include/kdb_lz4.h"
+#include "crc_device.h"
 #include "lz4_device.h"
 
 namespace kdb_lz4 {
@@ -52,49 +53,6 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(const uint32_t* __restr
 namespace {
 
 constexpr uint32_t kEntryFull = 0x8, kUncompacted = 0x2, kHasPadding = 0x4;   // format.h:34-42
-
-// ----------------------------------------------------------------- CRC32C
-// Reflected Castagnoli (crc32c.cc:296-340).  Tables built at compile time:
-//   kCrcT[b]        one-byte step of the table-driven loop;
-//   kShift[k][b]    column b of the GF(2) matrix that advances a raw CRC
-//                   register over 2^k zero bytes (matrix squaring).
-struct CrcTables {
-  uint32_t t[256];
-  uint32_t shift[32][32];
-};
-constexpr CrcTables make_crc_tables() {
-  CrcTables c{};
-  for (uint32_t i = 0; i < 256; i++) {
-    uint32_t v = i;
-    for (int k = 0; k < 8; k++) v = (v >> 1) ^ (0x82F63B78u & (0u - (v & 1u)));
-    c.t[i] = v;
-  }
-  for (int b = 0; b < 32; b++) {
-    const uint32_t v = 1u << b;
-    c.shift[0][b] = c.t[v & 0xffu] ^ (v >> 8);
-  }
-  for (int k = 1; k < 32; k++)
-    for (int b = 0; b < 32; b++) {
-      uint32_t v = c.shift[k - 1][b], r = 0;
-      for (int j = 0; j < 32; j++)
-        if ((v >> j) & 1u) r ^= c.shift[k - 1][j];
-      c.shift[k][b] = r;
-    }
-  return c;
-}
-__constant__ CrcTables kCrc = make_crc_tables();
-
-// Four bytes whose raw CRC (register 0 in) is 0xFFFFFFFF: prepending them to a
-// message makes the raw CRC equal the conditioned one's pre-xorout value, so
-// leading zero bytes (raw CRC 0) can pad every message to 64 equal lane chunks.
-constexpr uint32_t kCrcPrefix = 0x641F6454u;
-
-__device__ __forceinline__ uint32_t crc_shift(uint32_t c, uint32_t k) {   // advance over 2^k zero bytes
-  uint32_t r = 0;
-#pragma unroll
-  for (int b = 0; b < 32; b++) r ^= ((c >> b) & 1u) ? kCrc.shift[k][b] : 0u;
-  return r;
-}
 
 // ----------------------------------------------------------------- hashes
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
@@ -384,6 +342,28 @@ struct PartSrc {
   }
 };
 
+// The CRC's message: the key, then every chunk_final back to back.
+struct PutMsg {
+  const uint8_t* key;
+  uint32_t klen;
+  PartSrc src;
+  const uint32_t* plen;
+  uint32_t p0, p1;
+  __device__ uint32_t feed(uint64_t a, uint64_t b, uint32_t c, const uint32_t* s_t) const {
+    uint64_t m = a;
+    for (; m < b && m < klen; m++) c = crc::step(c, key[m], s_t);
+    if (m >= b) return c;
+    uint64_t j = m - klen, base = 0;
+    uint32_t p = p0;
+    while (p < p1 && j >= base + plen[p]) { base += plen[p]; p++; }
+    for (; m < b; m++, j++) {
+      while (p < p1 && j >= base + plen[p]) { base += plen[p]; p++; }
+      c = crc::step(c, src.byte(p, j - base), s_t);
+    }
+    return c;
+  }
+};
+
 constexpr int kEntryBlock = 256;
 
 // Wave per value: entry bytes at entries + entry_off[v].
@@ -396,7 +376,7 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
     uint32_t* __restrict__ kind_out, int32_t* __restrict__ status_out) {
   __shared__ uint32_t s_t[256];
   __shared__ uint8_t s_hdr[kEntryBlock / 64][64];
-  for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_t[i] = kCrc.t[i];
+  crc::stage_table(s_t);
   __syncthreads();
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x / 64u;
@@ -426,44 +406,9 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
     const uint64_t region = (uint64_t)entry_len[v] - hl - klen;
     for (uint64_t j = L.stored + lane; j < region; j += 64u) vdst[j] = 0;
 
-    // CRC32C(key || every chunk_final): 64 lane chunks of Lc bytes over
-    // zeros(z) || kCrcPrefix || message, combined in a 6-level tree.
-    const uint64_t mlen = (uint64_t)klen + L.crc_bytes;
-    uint32_t lg = 0;
-    while ((64ull << lg) < mlen + 4u) lg++;
-    const uint64_t Lc = 1ull << lg;
-    const uint64_t z = 64ull * Lc - (mlen + 4u);
-    uint32_t c = 0;
-    {
-      uint64_t pos = (uint64_t)lane * Lc;          // position in the padded message
-      const uint64_t end = pos + Lc;
-      if (end > z) {
-        if (pos < z) pos = z;
-        // part cursor for message byte m = pos - z - 4 (>= klen: chunk_final bytes)
-        uint32_t cp = p0;
-        uint64_t cbase = 0;   // crc-span offset where part cp starts
-        for (; pos < end; pos++) {
-          const int64_t m = (int64_t)(pos - z) - 4;
-          uint32_t b;
-          if (m < 0) {
-            b = (kCrcPrefix >> (8u * (uint32_t)(m + 4))) & 0xffu;
-          } else if ((uint64_t)m < klen) {
-            b = key[m];
-          } else {
-            const uint64_t j = (uint64_t)m - klen;
-            while (cp < p1 && j >= cbase + plen[cp]) { cbase += plen[cp]; cp++; }
-            b = src.byte(cp, j - cbase);
-          }
-          c = s_t[(c ^ b) & 0xffu] ^ (c >> 8);
-        }
-      }
-    }
-#pragma unroll
-    for (uint32_t s = 0; s < 6; s++) {
-      const uint32_t other = (uint32_t)__shfl_xor((int)c, 1 << s);
-      if ((lane & (1u << s)) == 0) c = crc_shift(c, lg + s) ^ other;
-    }
-    const uint32_t crc = uni(c) ^ 0xFFFFFFFFu;
+    // CRC32C(key || every chunk_final) (database.cc:251-257), on the wave
+    const PutMsg msg{key, klen, src, plen, p0, p1};
+    const uint32_t crc = crc::extend_wave(0u, (uint64_t)klen + L.crc_bytes, msg, s_t);
 
     if (lane == 0) {
       const uint64_t h = hash_type == 1 ? xxh64(key, klen) : murmur3_64(key, klen);

@@ -72,6 +72,9 @@ class Oracle:
                                       _u8p, ctypes.POINTER(c.c_uint64), ctypes.POINTER(c.c_uint32),
                                       ctypes.POINTER(c.c_uint64), ctypes.POINTER(c.c_uint32)]
         lib.orc_put_value.restype = c.c_int
+        lib.orc_get_value.argtypes = [_u8p, c.c_uint64, c.c_uint64, c.c_uint64, c.c_uint32, c.c_uint32, c.c_int, _u8p,
+                                      ctypes.POINTER(c.c_uint64)]
+        lib.orc_get_value.restype = c.c_int
         self.lib = lib
 
     def compress_bound(self, n: int) -> int:
@@ -136,6 +139,17 @@ class Oracle:
     def padding(self, size_value: int) -> int:
         return self.lib.orc_padding(size_value)
 
+    def get_value(self, stored: bytes, svc: int, size: int, checksum: int = 0, checksum_initial: int = 0,
+                  verify: int = 0) -> tuple[int, bytes]:
+        """CompressorLZ4::UncompressByteArray of one stored value: (status, defined output bytes)."""
+        src = np.zeros(len(stored) + 64, np.uint8)
+        src[: len(stored)] = np.frombuffer(stored, np.uint8)
+        out = np.zeros(size + 64, np.uint8)
+        n = ctypes.c_uint64(0)
+        st = self.lib.orc_get_value(_ptr(src), len(stored), svc, size, checksum, checksum_initial, verify, _ptr(out),
+                                    ctypes.byref(n))
+        return st, out[: n.value].tobytes()
+
     def put_value(self, key: bytes, value: bytes, chunks: list[int] | None = None) -> dict:
         """Database::PutPart over `chunks` (default: one chunk) of one value:
         {"parts": [(offset_chunk_compressed, chunk_final bytes)], "svc", "crc",
@@ -177,6 +191,9 @@ class Reference:
         lib.ref_frames_uncompress.restype = c.c_int64
         lib.ref_crc32c_extend.argtypes = [c.c_uint32, _u8p, c.c_uint64]
         lib.ref_crc32c_extend.restype = c.c_uint32
+        lib.ref_uncompress_value.argtypes = [_u8p, c.c_uint64, c.c_uint64, c.c_uint64, c.c_uint32, c.c_uint32,
+                                             c.c_int, _u8p, ctypes.POINTER(c.c_uint64)]
+        lib.ref_uncompress_value.restype = c.c_int
         lib.ref_gen_g2.argtypes = [_u8p, c.c_int, c.c_int]
         lib.ref_gen_g3.argtypes = [_u8p, c.c_int, c.c_int]
         self.lib = lib
@@ -215,6 +232,16 @@ class Reference:
     def crc32c(self, data: bytes, crc: int = 0) -> int:
         a = np.frombuffer(data, dtype=np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
         return self.lib.ref_crc32c_extend(crc, _ptr(a), len(data))
+
+    def uncompress_value(self, stored: bytes, svc: int, size: int, checksum: int = 0, checksum_initial: int = 0,
+                         verify: bool = False) -> tuple[int, bytes]:
+        """CompressorLZ4::UncompressByteArray: (0 OK / 1 Invalid checksum / 2 IOError, value bytes)."""
+        src = np.frombuffer(stored, np.uint8).copy() if len(stored) else np.zeros(1, np.uint8)
+        out = np.zeros(size + 64, np.uint8)
+        n = ctypes.c_uint64(0)
+        st = self.lib.ref_uncompress_value(_ptr(src), len(stored), svc, size, checksum, checksum_initial,
+                                           1 if verify else 0, _ptr(out), ctypes.byref(n))
+        return st, out[: n.value].tobytes()
 
     def g2(self, size: int, count: int) -> np.ndarray:
         out = np.empty(size * count, dtype=np.uint8)

@@ -524,6 +524,79 @@ int orc_put_value(const uint8_t* key, uint32_t klen, const uint8_t* value, uint6
   return 0;
 }
 
+/*
+ * CompressorLZ4::UncompressByteArray (algorithm/compressor.cc:140-249) over
+ * CompressorLZ4::Uncompress (compressor.cc:75-137): the read of one stored
+ * value (Database::GetRaw, interface/database.cc:65-68).  `stored` holds
+ * `avail` readable bytes (the entry's value region); svc = size_value_compressed
+ * (0: the value is not compressed), size = size_value.  verify: 0 none,
+ * 1 the reference's checksum check -- each frame streamed into the CRC twice,
+ * Uncompress (:126) and UncompressByteArray (:202) -- 2 the same with each frame
+ * streamed once (the corrected check).  Returns 0 OK, -1 IOError from the
+ * block decoder, -2 IOError "Invalid checksum.", -3 where the reference would
+ * read or write outside the value (malformed sizes; undefined there).
+ * *out_n = bytes of `out` the reference defines.
+ */
+int orc_get_value(const uint8_t* stored, uint64_t avail, uint64_t svc, uint64_t size, uint32_t checksum,
+                  uint32_t checksum_initial, int verify, uint8_t* out, uint64_t* out_n) {
+  uint32_t crc = verify ? checksum_initial : 0;                  /* :144-147 */
+  const int compressed = svc != 0;
+  int disabled = 0;
+  uint64_t in = 0, o = 0;
+  *out_n = 0;
+  for (;;) {
+    if (compressed && !disabled) {
+      if (in == svc) {                                           /* :159-169 */
+        if (!verify || crc == checksum) return 0;
+        return -2;
+      }
+      if (in > svc || in + 8 > avail) return -3;
+      int zero = 1;                                              /* HasFrameHeaderDisabledCompression */
+      for (int i = 0; i < 8; i++) zero &= stored[in + i] == 0;
+      if (zero) {                                                /* :171-178 */
+        disabled = 1;
+        if (verify) crc = orc_crc32c_extend(crc, stored + in, 8);
+        in += 8;
+      } else {
+        uint32_t st = rd32(stored + in), raw = rd32(stored + in + 4);
+        uint64_t fsz;
+        if (o + raw > size) return -3;
+        if (st > 0) {                                            /* :92-113 */
+          uint32_t csz = st - 8;                                 /* u32 wrap below 8 */
+          if ((int)csz < 0) return -1;  /* negative block size: the r1.3.0 decoder fails at its first check */
+          if ((uint64_t)csz + 8 > avail - in) return -3;
+          int ret = orc_decompress_safe_partial(stored + in + 8, out + o, (int)csz, (int)raw, (int)raw);
+          if (ret <= 0) return -1;
+          fsz = (uint64_t)csz + 8;
+          o += (uint64_t)ret;
+        } else {                                                 /* :114-121 */
+          if ((uint64_t)raw + 8 > avail - in) return -3;
+          memcpy(out + o, stored + in + 8, raw);
+          fsz = (uint64_t)raw + 8;
+          o += raw;
+        }
+        if (verify) {                                            /* :126 (+ :202) */
+          crc = orc_crc32c_extend(crc, stored + in, fsz);
+          if (verify == 1) crc = orc_crc32c_extend(crc, stored + in, fsz);
+        }
+        in += fsz;
+        *out_n = o;
+      }
+    }
+    if (!compressed || disabled) {                               /* :224-247 */
+      const uint64_t left = compressed ? svc : size;
+      if (in == left) return 0;
+      if (in > left) return -3;
+      uint64_t cur = left - in < 1048576u ? left - in : 1048576u;
+      if (in + cur > avail || o + cur > size) return -3;
+      memcpy(out + o, stored + in, cur);
+      o += cur;
+      *out_n = o;
+      return 0;
+    }
+  }
+}
+
 /* ---- Generators ----------------------------------------------------------
  * G1: db_bench's RandomGenerator (doc/bench/db_bench_kingdb.cc:113-142) over
  * LevelDB's Random(301) (Park-Miller, A=16807, M=2^31-1) and

@@ -162,3 +162,38 @@ extern "C" int ref_bench_roundtrip(const char* src, int n, int size, int threads
   if (memcmp(out.data(), src, (size_t)n * size) != 0) bad = 1;
   return bad ? -1 : 0;
 }
+
+// ByteArray's size/checksum setters are private to KingDB's own classes; the
+// shim reaches them through one of the befriended names (NetworkTask lives in
+// network/server.h, which is not part of this build), exactly as
+// StorageEngine::GetEntry sets them (storage/storage_engine.h:497-508).
+namespace kdb {
+class NetworkTask {
+ public:
+  static void Set(ByteArray& v, uint64_t size, uint64_t svc, uint32_t checksum, uint32_t checksum_initial) {
+    v.set_size(size);
+    v.set_size_compressed(svc);
+    v.set_checksum(checksum);
+    v.set_checksum_initial(checksum_initial);
+  }
+};
+}  // namespace kdb
+
+// CompressorLZ4::UncompressByteArray (compressor.cc:140-249) on a stored value
+// region, as Database::GetRaw calls it (database.cc:65-68).  Returns 0 OK,
+// 1 IOError "Invalid checksum.", 2 any other IOError; *out_n = value size.
+extern "C" int ref_uncompress_value(const char* stored, uint64_t stored_len, uint64_t svc, uint64_t size,
+                                    uint32_t checksum, uint32_t checksum_initial, int verify, char* out,
+                                    uint64_t* out_n) {
+  std::vector<char> buf(stored_len + 64, 0);
+  if (stored_len) memcpy(buf.data(), stored, stored_len);
+  kdb::ByteArray v = kdb::NewDeepCopyByteArray(buf.data(), stored_len + 64);
+  kdb::NetworkTask::Set(v, size, svc, checksum, checksum_initial);
+  kdb::CompressorLZ4 c;
+  kdb::ByteArray o;
+  kdb::Status s = c.UncompressByteArray(v, verify != 0, &o);
+  *out_n = o.size();
+  if (o.size()) memcpy(out, o.data(), o.size());
+  if (s.IsOK()) return 0;
+  return s.ToString().find("Invalid checksum") != std::string::npos ? 1 : 2;
+}

@@ -15,7 +15,7 @@ def header_symbols():
     for h in ("kdb_lz4.h", "kdb_put.h"):
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-        syms |= set(re.findall(r"\b(kdb_(?:lz4|put|hstable)_\w+)\s*\(", text))
+        syms |= set(re.findall(r"\b(kdb_(?:lz4|put|get|hstable)_\w+)\s*\(", text))
     return sorted(syms)
 
 
