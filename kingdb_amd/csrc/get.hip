@@ -40,8 +40,7 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
                              uint8_t* dst, const uint64_t* dst_off, const uint32_t* out_cap,
                              const uint32_t* target, uint32_t* out_len, int32_t* ret);
-__global__ __launch_bounds__(1024) void pack_scan_kernel(const uint32_t* __restrict__ len, uint32_t n,
-                                                         uint64_t* __restrict__ dst_off, uint64_t* __restrict__ total);
+hipError_t launch_exclusive_scan(hipStream_t st, const uint32_t* len, uint32_t n, uint64_t* off, uint64_t* total);
 
 namespace {
 
@@ -262,7 +261,10 @@ hipError_t launch_get_values(hipStream_t st, const uint8_t* stored, const uint64
   if (n == 0) return hipSuccess;
   const uint32_t tb = 256, tg = (n + tb - 1) / tb < 4096u ? (n + tb - 1) / tb : 4096u;
   hipLaunchKernelGGL(get_count_kernel, dim3(tg), dim3(tb), 0, st, stored, stored_off, avail, svc, size, n, nframes);
-  hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, st, nframes, n, frame_first, total);
+  {
+    const hipError_t e = launch_exclusive_scan(st, nframes, n, frame_first, total);
+    if (e != hipSuccess) return e;
+  }
   // The frame count is only known on the device, so the decode launch covers
   // the whole capacity; slots the walk leaves empty stay inert: offset 0 (the
   // first stored bytes, always readable), 0 bytes available and 0 output bytes

@@ -426,7 +426,9 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
-    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
+    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
+    uint32_t cls) {
+  if (census && census[cls] == 0) return;      // no value of this size class in the batch
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
@@ -541,7 +543,9 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    const uint32_t* __restrict__ census, uint32_t cls) {
+  if (census && census[cls] == 0) return;      // no value of this size class in the batch
   __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
   const uint32_t lane = lane_id();
   // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
@@ -605,11 +609,28 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   }
 }
 
+// Values per size class (len <= b0, <= b1, <= b2, above), so that a class
+// launch with nothing to do returns at once instead of scanning the batch.
+__global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n, uint32_t b0, uint32_t b1,
+                                    uint32_t b2, uint32_t* __restrict__ counts) {
+  uint32_t c[4] = {0, 0, 0, 0};
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+    const uint32_t L = len[v];
+    c[L <= b0 ? 0 : L <= b1 ? 1 : L <= b2 ? 2 : 3]++;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint32_t x = c[k];
+    for (int d = 32; d >= 1; d >>= 1) x += (uint32_t)__shfl_xor((int)x, d);
+    if (lane_id() == 0 && x) atomicAdd(&counts[k], x);
+  }
+}
+
 template <bool F, bool Sm>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
-                             int32_t* ret) {
+                             int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0) {
   auto kern = lz4_compress_kernel<F, Sm>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
@@ -617,14 +638,15 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
-                     dst_cap, frame_len, ret, work, batch);
+                     dst_cap, frame_len, ret, work, batch, census, cls);
   return hipGetLastError();
 }
 
 template <bool F, bool W>
 static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                              uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst, const uint64_t* dst_off,
-                             const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret) {
+                             const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret,
+                             const uint32_t* census = nullptr, uint32_t cls = 0) {
   auto kern = lz4_compress_big_kernel<F, W>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
@@ -632,7 +654,7 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
   const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
-                     dst_cap, frame_len, ret, work, batch);
+                     dst_cap, frame_len, ret, work, batch, census, cls);
   return hipGetLastError();
 }
 
@@ -645,15 +667,27 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                            int32_t* ret) {
   if (n == 0) return hipSuccess;
   hipError_t e;
+  static const uint32_t mid_split_env = [] {
+    const char* v = getenv("KDB_LZ4_CSPLIT");
+    return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : kMidLdsMax;
+  }();
+  uint32_t* census = nullptr;            // per-class counts, when more than one class may launch
+  if (max_len > kSmallMax) {
+    e = work_counter(st, &census);
+    if (e != hipSuccess) return e;
+    const uint32_t b1 = min(max(mid_split_env, kSmallMax), k64KLimit - 1u);
+    hipLaunchKernelGGL(class_census_kernel, dim3(min((n + 255u) / 256u, 1024u)), dim3(256), 0, st, src_len, n,
+                       kSmallMax, b1, k64KLimit - 1u, census);
+  }
   {
     size_t lds = compress_lds_bytes(kSmallMax);
 #ifdef KDB_ABL_OCC
     lds = 163840 / KDB_ABL_OCC;   // diagnostic: force KDB_ABL_OCC workgroups per CU
 #endif
     e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                       frame_len, ret)
+                                       frame_len, ret, census, 0)
               : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                        frame_len, ret);
+                                        frame_len, ret, census, 0);
     if (e != hipSuccess) return e;
   }
   // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
@@ -667,24 +701,25 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     const uint32_t hi = min(min(max_len, mid_split), k64KLimit - 1u);
     const size_t lds = compress_lds_bytes(hi);
     e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
-                                        dst_cap, frame_len, ret)
+                                        dst_cap, frame_len, ret, census, 1)
               : launch_one<false, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
-                                         dst_cap, frame_len, ret);
+                                         dst_cap, frame_len, ret, census, 1);
     if (e != hipSuccess) return e;
   }
   const uint32_t glo = max(mid_split, kSmallMax) + 1u;
   if (max_len >= glo && glo < k64KLimit) {
     const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
-    e = frame ? launch_big<true, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len, ret)
+    e = frame ? launch_big<true, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len, ret,
+                                        census, 2)
               : launch_big<false, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
-                                         ret);
+                                         ret, census, 2);
     if (e != hipSuccess) return e;
   }
   if (max_len >= k64KLimit)
     e = frame ? launch_big<true, true>(st, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
-                                       frame_len, ret)
+                                       frame_len, ret, census, 3)
               : launch_big<false, true>(st, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
-                                        frame_len, ret);
+                                        frame_len, ret, census, 3);
   return e;
 }
 

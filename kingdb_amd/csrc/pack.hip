@@ -12,6 +12,10 @@
 //   2. pack_copy_kernel: one wave per value, dword-aligned stores on the
 //      destination side (alignbyte of two aligned source dwords), byte stores
 //      only at the ragged ends.  HBM-bound: 2*ΣF bytes.
+#include <atomic>
+#include <mutex>
+#include <unordered_map>
+
 #include "lz4_device.h"
 #include "kdb_lz4.h"
 
@@ -44,6 +48,125 @@ __global__ __launch_bounds__(kScanThreads) void pack_scan_kernel(const uint32_t*
     run += len[i];
   }
   if (t == kScanThreads - 1) *total = part[t];
+}
+
+// ---------------------------------------------------------------------------
+// Device-wide exclusive scan of u32 lengths into u64 offsets (+ total), in
+// three launches: per-block sums, a scan of the block sums (one block), then
+// the per-block scan with its block's base.  A block covers kScanTile
+// elements (16 per thread).  The block sums live in a per-device ring of
+// scratch slots (one per launch, reused after kScanSlots later launches, like
+// the work counters); inputs past kScanSlotSums blocks fall back to the
+// single-workgroup kernel above.
+constexpr uint32_t kScanBlock = 256, kScanPer = 16, kScanTile = kScanBlock * kScanPer;
+constexpr uint32_t kScanSlots = 1024, kScanSlotSums = 1024;   // <= 4 Mi elements per scan
+
+__device__ __forceinline__ uint64_t block_exclusive(uint64_t v, uint64_t* sh, uint64_t* total) {
+  // exclusive scan of one u64 per thread over the block (wave shuffles + LDS)
+  const uint32_t t = threadIdx.x, lane = lane_id(), w = t / 64u;
+  uint64_t x = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  uint64_t base = 0, all = 0;
+  for (uint32_t k = 0; k < kScanBlock / 64u; k++) {
+    if (k < w) base += sh[k];
+    all += sh[k];
+  }
+  __syncthreads();
+  *total = all;
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(const uint32_t* __restrict__ len, uint32_t n,
+                                                                 uint64_t* __restrict__ sums) {
+  __shared__ uint64_t sh[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; k++)
+    if (base + k < n) s += len[base + k];
+  uint64_t tot;
+  block_exclusive(s, sh, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_top_kernel(uint64_t* __restrict__ sums, uint32_t nb,
+                                                                uint64_t* __restrict__ total) {
+  __shared__ uint64_t sh[kScanBlock / 64];
+  // nb <= kScanSlotSums: at most 4 sums per thread
+  const uint32_t per = (nb + kScanBlock - 1) / kScanBlock;
+  const uint32_t lo = threadIdx.x * per;
+  uint64_t s = 0;
+  for (uint32_t k = 0; k < per; k++)
+    if (lo + k < nb) s += sums[lo + k];
+  uint64_t tot;
+  uint64_t run = block_exclusive(s, sh, &tot);
+  for (uint32_t k = 0; k < per; k++)
+    if (lo + k < nb) {
+      const uint64_t v = sums[lo + k];
+      sums[lo + k] = run;
+      run += v;
+    }
+  if (threadIdx.x == 0) *total = tot;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint32_t* __restrict__ len, uint32_t n,
+                                                                  const uint64_t* __restrict__ sums,
+                                                                  uint64_t* __restrict__ off) {
+  __shared__ uint64_t sh[kScanBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  uint32_t v[kScanPer];
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; k++) {
+    v[k] = base + k < n ? len[base + k] : 0u;
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t run = sums[blockIdx.x] + block_exclusive(s, sh, &tot);
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; k++)
+    if (base + k < n) {
+      off[base + k] = run;
+      run += v[k];
+    }
+}
+
+namespace {
+std::mutex g_scan_mu;
+std::unordered_map<int, std::pair<uint64_t*, std::atomic<uint32_t>*>> g_scan_pools;
+}  // namespace
+
+hipError_t launch_exclusive_scan(hipStream_t st, const uint32_t* len, uint32_t n, uint64_t* off, uint64_t* total) {
+  const uint32_t nb = (n + kScanTile - 1) / kScanTile;
+  if (n == 0) return hipMemsetAsync(total, 0, 8, st);
+  if (nb > kScanSlotSums) {
+    hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, len, n, off, total);
+    return hipGetLastError();
+  }
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  uint64_t* slot;
+  {
+    std::lock_guard<std::mutex> l(g_scan_mu);
+    auto& p = g_scan_pools[dev];
+    if (!p.first) {
+      e = hipMalloc(&p.first, (size_t)kScanSlots * kScanSlotSums * 8u);
+      if (e != hipSuccess) return e;
+      p.second = new std::atomic<uint32_t>(0);
+    }
+    slot = p.first + (size_t)(p.second->fetch_add(1) % kScanSlots) * kScanSlotSums;
+  }
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(nb), dim3(kScanBlock), 0, st, len, n, slot);
+  hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanBlock), 0, st, slot, nb, total);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kScanBlock), 0, st, len, n, slot, off);
+  return hipGetLastError();
 }
 
 __device__ __forceinline__ uint32_t ld32a(const uint8_t* p) { return *(const uint32_t*)p; }
@@ -91,8 +214,7 @@ extern "C" int kdb_lz4_pack_frames(void* stream, const uint8_t* src, const uint6
   if ((n && (!src || !src_off || !len || !dst || !dst_off)) || !total) return KDB_LZ4_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (n == 0) return hipMemsetAsync(total, 0, 8, st) == hipSuccess ? KDB_LZ4_OK : KDB_LZ4_EHIP;
-  hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, len, n, dst_off, total);
-  if (hipGetLastError() != hipSuccess) return KDB_LZ4_EHIP;
+  if (launch_exclusive_scan(st, len, n, dst_off, total) != hipSuccess) return KDB_LZ4_EHIP;
   const uint32_t waves = n < 65536u ? n : 65536u;
   hipLaunchKernelGGL(pack_copy_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, src, src_off, len, n, dst,
                      dst_off);

@@ -24,7 +24,7 @@
 //
 // Pipeline (stream-ordered; every kernel reads only what earlier ones wrote):
 //   put_prep_kernel     thread per value: each part's raw offset and frame slot size
-//   scan                frame slot offsets (pack_scan_kernel)
+//   scan                frame slot offsets (launch_exclusive_scan, pack.hip)
 //   frame compress      the LZ4 kernels over every part (launch_compress)
 //   put_policy_kernel   thread per value: the frame policy and the entry layout
 //   scan                dense entry offsets
@@ -47,8 +47,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                            const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret);
-__global__ __launch_bounds__(1024) void pack_scan_kernel(const uint32_t* __restrict__ len, uint32_t n,
-                                                         uint64_t* __restrict__ dst_off, uint64_t* __restrict__ total);
+hipError_t launch_exclusive_scan(hipStream_t st, const uint32_t* len, uint32_t n, uint64_t* off, uint64_t* total);
 
 namespace {
 
@@ -375,8 +374,10 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
     const uint32_t* __restrict__ entry_len, uint64_t* __restrict__ hashed, uint32_t* __restrict__ crc_out,
     uint32_t* __restrict__ kind_out, int32_t* __restrict__ status_out) {
   __shared__ uint32_t s_t[256];
+  __shared__ uint8_t s_c8[256];
   __shared__ uint8_t s_hdr[kEntryBlock / 64][64];
   crc::stage_table(s_t);
+  for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_c8[i] = kCrc8.t[i];
   __syncthreads();
   const uint32_t lane = lane_id();
   const uint32_t wib = threadIdx.x / 64u;
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
       q = put_varint(q, L.pad_hdr);
       for (int i = 0; i < 8; i++) *q++ = (uint8_t)(h >> (8 * i));
       uint32_t c8 = 0xffu;                        // crc8(0, header + 1, hl - 1)
-      for (uint32_t i = 1; i < hl; i++) c8 = kCrc8.t[(c8 ^ hdr[i]) & 0xffu];
+      for (uint32_t i = 1; i < hl; i++) c8 = s_c8[(c8 ^ hdr[i]) & 0xffu];
       hdr[0] = (uint8_t)(c8 ^ 0xffu);
     }
     __builtin_amdgcn_wave_barrier();
@@ -482,14 +483,18 @@ hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_
   hipLaunchKernelGGL(put_prep_kernel, dim3(tg), dim3(tb), 0, st, value_off, part_first, chunk_len, n, part_src,
                      part_slot);
   if (nparts) {
-    hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, st, part_slot, nparts, frame_off, ftotal);
-    hipError_t e = launch_compress(true, st, values, part_src, chunk_len, nparts, max_chunk, frames, frame_off,
+    hipError_t e = launch_exclusive_scan(st, part_slot, nparts, frame_off, ftotal);
+    if (e != hipSuccess) return e;
+    e = launch_compress(true, st, values, part_src, chunk_len, nparts, max_chunk, frames, frame_off,
                                    nullptr, frame_len, fstatus);
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(put_policy_kernel, dim3(tg), dim3(tb), 0, st, key_len, value_len, part_first, chunk_len,
                      frame_len, fstatus, n, occ, plen, mode, lay, entry_len);
-  hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, st, entry_len, n, entry_off, total);
+  {
+    const hipError_t e = launch_exclusive_scan(st, entry_len, n, entry_off, total);
+    if (e != hipSuccess) return e;
+  }
   const uint32_t eg = (n + 3) / 4 < 16384u ? (n + 3) / 4 : 16384u;
   PartSrc ps{values, frames, part_src, frame_off, mode};
   hipLaunchKernelGGL(put_entry_kernel, dim3(eg), dim3(kEntryBlock), 0, st, keys, key_off, key_len, value_len,

@@ -189,6 +189,32 @@ def test_device_batch_mixed_config4(gpu, orc):
     b.free()
 
 
+def test_device_scan_sizes(gpu):
+    """launch_exclusive_scan (three-launch multi-block scan, pack.hip) at tile
+    edges, and its single-workgroup fallback past 4 Mi elements, through
+    kdb_lz4_pack_frames' offsets and total."""
+    from kingdb_amd import _lib
+    from kingdb_amd.lz4 import DeviceBuffer, lib
+    rng = np.random.default_rng(4)
+    for n in (1, 4095, 4096, 4097, 70001, (4 << 20) + 5):
+        lens = rng.integers(0, 8, n).astype(np.uint32)
+        src = DeviceBuffer(n * 8 + 64)
+        src.upload(rng.integers(0, 256, n * 8, dtype=np.uint8))
+        so = DeviceBuffer(8 * n)
+        so.upload(np.arange(n, dtype=np.uint64) * 8)
+        ln = DeviceBuffer(4 * n)
+        ln.upload(lens)
+        dst = DeviceBuffer(int(lens.sum()) + 64)
+        doff = DeviceBuffer(8 * n)
+        tot = DeviceBuffer(8)
+        _lib.check(lib().kdb_lz4_pack_frames(None, src.ptr, so.ptr, ln.ptr, n, dst.ptr, doff.ptr, tot.ptr), "pack")
+        exp = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))])
+        assert np.array_equal(doff.download(8 * n).view(np.uint64), exp[:-1]), n
+        assert int(tot.download(8).view(np.uint64)[0]) == int(exp[-1]), n
+        for b in (src, so, ln, dst, doff, tot):
+            b.free()
+
+
 def test_pack_frames(gpu):
     """kdb_lz4_pack_frames: ragged lengths, unaligned source and destination."""
     from kingdb_amd import lz4 as L
