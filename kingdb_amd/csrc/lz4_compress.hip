@@ -242,12 +242,23 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         lo = hi = 0u;
 #else
 #pragma unroll
-        for (int bb = 0; bb < kHashBits; ++bb) {
-          const uint32_t t = (uint32_t)((int32_t)(h << (31 - bb)) >> 31);   // 0 or ~0
-          const uint64_t m = ballot(t != 0u);
+        for (int bb = 0; bb < kHashBits; bb += 2) {
+          // t = 0 or ~0 (one v_bfe_i32); the empty asm keeps the ballot on t
+          // itself instead of a second shift + compare of h.  Bits go in pairs
+          // so each ballot's SGPR write is not read by the very next VALU op
+          // (no s_nop wait states).
+          uint32_t t0 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb, 1);
+          uint32_t t1 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb + 1 < kHashBits ? bb + 1 : bb, 1);
+          asm volatile("" : "+v"(t0), "+v"(t1));
+          const uint64_t m0 = ballot(t0 != 0u);
+          const uint64_t m1 = ballot(t1 != 0u);
           // acc & ~(t ^ m) in one v_bitop3 per half (truth table 0x90)
-          lo = __builtin_amdgcn_bitop3_b32(lo, t, (uint32_t)m, 0x90);
-          hi = __builtin_amdgcn_bitop3_b32(hi, t, (uint32_t)(m >> 32), 0x90);
+          lo = __builtin_amdgcn_bitop3_b32(lo, t0, (uint32_t)m0, 0x90);
+          hi = __builtin_amdgcn_bitop3_b32(hi, t0, (uint32_t)(m0 >> 32), 0x90);
+          if (bb + 1 < kHashBits) {
+            lo = __builtin_amdgcn_bitop3_b32(lo, t1, (uint32_t)m1, 0x90);
+            hi = __builtin_amdgcn_bitop3_b32(hi, t1, (uint32_t)(m1 >> 32), 0x90);
+          }
         }
 #endif
         const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;

@@ -82,12 +82,12 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
     const int cpy = op + length;                                  // lz4.cc:930-952
     const bool last = cpy > oexit || ip + length > iend - (int)(2 + 1 + kLastLiterals);
     if (last && (cpy > oend || ip + length > iend)) return -ip - 1;
+    // Whole 64-byte steps, no lane mask: the bytes written past the run land
+    // in output the decoder has not produced yet (overwritten before anything
+    // reads them; the window has 64 bytes of slack) -- no exec-mask juggling
+    // on the scalar unit, which is what this loop is bound by.
 #pragma unroll 1
-    for (int i = 0; i < length; i += 64) {
-      const int j = i + (int)lane;
-      const uint8_t b = in[ip + j];
-      if (j < length) out[op + j] = b;
-    }
+    for (int i = 0; i < length; i += 64) out[op + i + (int)lane] = in[ip + i + (int)lane];
     ip += length;
     op = cpy;
     if (last) break;
@@ -115,12 +115,12 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
     if (op + mlen > oend - (int)kLastLiterals) return -ip - 1;    // lz4.cc:1024
     asm volatile("" ::: "memory");
     if (off >= mlen || off >= 64) {
-      // plain forward copy in 64-byte steps: every source byte is < the step
+      // plain forward copy in 64-byte steps: every source byte a lane < mlen
+      // reads is < the step (lanes past mlen write the not-yet-produced tail)
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
-        const int j = i + (int)lane;
-        const uint8_t b = out[ref + j];
-        if (j < mlen) out[op + j] = b;
+        const uint8_t b = out[ref + i + (int)lane];
+        out[op + i + (int)lane] = b;
         asm volatile("" ::: "memory");
       }
     } else if (off > 0) {
@@ -130,9 +130,8 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
-        const int j = i + (int)lane;
         const uint8_t b = out[ref + i + rr];
-        if (j < mlen) out[op + j] = b;
+        out[op + i + (int)lane] = b;
       }
     }  // off == 0: the reference copies the destination onto itself
     asm volatile("" ::: "memory");
@@ -156,9 +155,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     uint32_t skip_big) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
-  const uint32_t out_bytes = ((out_cap_max + 15u) & ~15u) + 16u;
-  uint8_t* s_out = smem;
-  uint8_t* s_in = smem + out_bytes;
+  // [staged block + 16 zero bytes][output window + 64 bytes of slack for the
+  // decoder's unmasked 64-byte steps]; the register window may read 256 bytes
+  // past the block, into the output window (decompress_lds_bytes)
+  uint8_t* s_in = smem;
+  uint8_t* s_out = smem + (((size_t)in_cap + 32u + 15u) & ~(size_t)15u);
 
   WorkQueue wq{work, n, batch, 0u, 0u};
 #pragma unroll 1
@@ -526,8 +527,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
 }
 
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
-  // out window | staged block + zero tail + the register window's 256-byte reach
-  return (((size_t)max_out + 15u) & ~(size_t)15u) + 16u + (((size_t)max_in + 15u) & ~(size_t)15u) + 320u;
+  // staged block (16 B alignment head + block + 16 zero bytes) | output window
+  // + 64 B slack; the register window reaches 256 B past the block
+  const size_t in_bytes = ((size_t)max_in + 32u + 15u) & ~(size_t)15u;
+  const size_t out_bytes = (((size_t)max_out + 15u) & ~(size_t)15u) + 64u;
+  return in_bytes + (out_bytes > 272u ? out_bytes : 272u);
 }
 
 template <bool F>

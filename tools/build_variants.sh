@@ -7,6 +7,6 @@ for v in "$@"; do
   name=${v%%:*}; flags=${v#*:}; [ "$flags" = "$v" ] && flags=""
   d=build/var_$name; mkdir -p $d
   for f in csrc/*.hip; do $H $flags -c $f -o $d/$(basename $f .hip).o & done; wait
-  /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -Icsrc -I../include -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -x c++ -c csrc/compressor.cc -o $d/compressor.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/var_$name.so $d/*.o -Wl,-rpath,/opt/rocm/lib
+  for f in csrc/*.cc; do /opt/rocm/bin/hipcc -O2 -std=c++17 -fPIC -Icsrc -I../include -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -x c++ -c $f -o $d/$(basename $f .cc).o; done
+  mkdir -p var && /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o var/var_$name.so $d/*.o -Wl,-rpath,/opt/rocm/lib
 done
