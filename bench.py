@@ -48,6 +48,9 @@ def parse():
                         "--values per GPU of 90%% 100 B / 9%% 4 KiB / 1%% 64 KiB parts, byte-balanced shards; "
                         "put: configs[4], --values puts per GPU of 16 B keys / 100 B values from pinned host "
                         "memory to HSTable file bytes in host memory")
+    p.add_argument("--put-host-copy", action="store_true",
+                   help="put workload: land entry bytes in a pinned staging buffer and memcpy them into the "
+                        "files (the default DMAs them from HBM straight into pinned file buffers)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU leg")
     p.add_argument("--no-verify", action="store_true")
@@ -152,6 +155,28 @@ def host_inclusive(batch, n: int, size: int, args) -> dict:
     return res
 
 
+def copy_bandwidth(batch, stream, reps: int = 5) -> float:
+    """Achievable HBM copy rate on this device: hipMemcpyAsync
+    device-to-device of the raw buffer, (read + write bytes) / time, HIP events
+    on the bench stream.  Run after the round trip was verified (it overwrites
+    the decoded output with the same bytes)."""
+    import kingdb_amd as K
+    from kingdb_amd import _lib
+    from kingdb_amd import lz4 as L
+    nb = int(batch.raw_bytes)
+
+    def cp():
+        _lib.check(L.lib().kdb_lz4_memcpy_d2d(batch.out.ptr, batch.src.ptr, nb, stream.ptr), "memcpy_d2d")
+    cp()
+    e0, e1 = K.Event(), K.Event()
+    e0.record(stream)
+    for _ in range(reps):
+        cp()
+    e1.record(stream)
+    ms = e0.elapsed_ms(e1) / reps
+    return 2.0 * nb / (ms * 1e-3) / 1e9
+
+
 def ref_write_path(keys: np.ndarray, vals: np.ndarray) -> dict | None:
     """configs[4] CPU path: the reference's own Database::PutPart -> WriteBuffer ->
     HSTableManager (oracle/_ref/ref_db, built from /root/reference) on the same
@@ -196,9 +221,9 @@ def bench_put(args, world: int, rank: int, local: int, barrier, sync_all) -> Non
     """configs[4]: the write path, host memory to HSTable bytes, PCIe included."""
     from kingdb_amd.lz4 import DeviceBuffer
     from kingdb_amd.putpipe import PutPipeline
-    from kingdb_amd.shard import max_over_ranks
+    from kingdb_amd.shard import gather_ranks, max_over_ranks
     n, ks, vs = args.values, 16, 100
-    pp = PutPipeline(n, ks, vs, chunk=args.hi_chunk, nstreams=args.hi_streams)
+    pp = PutPipeline(n, ks, vs, chunk=args.hi_chunk, nstreams=args.hi_streams, direct=not args.put_host_copy)
     base = rank * n                                   # this rank's slice of one global put sequence
     keys = np.frombuffer(b"".join(b"%016d" % (base + i) for i in range(n)), np.uint8).reshape(n, ks)
     pp.h_keys.np[:] = keys.reshape(-1)
@@ -218,7 +243,9 @@ def bench_put(args, world: int, rank: int, local: int, barrier, sync_all) -> Non
         times.append(pp.run())
     sync_all()
     barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine)
+    per_gpu = gather_ranks(n * args.steps / mine)
     # what was timed: every put accepted, entries framed in order (spot-check the
     # first entries' keys and sizes; byte parity is tests/test_write_path.py's job)
     files = pp.writer.files()
@@ -245,7 +272,9 @@ def bench_put(args, world: int, rank: int, local: int, barrier, sync_all) -> Non
         "config": {"workload": f"configs[4]: {n} puts per GPU through Database::PutPart semantics (frame policy, "
                                f"LZ4, CRC32C, xxHash-64, EntryHeader) into HSTable files, one writer per GPU",
                    "puts_per_gpu": n, "key_bytes": ks, "value_bytes": vs, "chunk": pp.chunk,
-                   "streams": len(pp.streams), "parallelism": f"dp{world} (independent shards, no collective)"},
+                   "streams": len(pp.streams), "entry_landing": "host copy" if args.put_host_copy else "direct DMA",
+                   "parallelism": f"dp{world} (independent shards, no collective)"},
+        "per_gpu_puts_per_s": [round(x, 1) for x in per_gpu],
         "mb_per_s_in": round(total * (ks + vs) / elapsed / 1e6, 1),
         "mb_per_s_out": round(file_bytes * max_over_ranks(1.0, op="sum") * args.steps / elapsed / 1e6, 1),
         "hstable_bytes_per_gpu": file_bytes, "files_per_gpu": len(files),
@@ -277,7 +306,7 @@ def main() -> None:
 
     import kingdb_amd as K
     from kingdb_amd import lz4 as L
-    from kingdb_amd.shard import g1_first_piece, max_over_ranks
+    from kingdb_amd.shard import g1_first_piece, gather_ranks, max_over_ranks
 
     K.set_device(local)
     torch_sync = torch.cuda.is_available()
@@ -333,8 +362,8 @@ def main() -> None:
     stream.sync()
     sync_all()
     barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed)
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine)
 
     c_ms = float(np.mean([evs[k][0].elapsed_ms(evs[k][1]) for k in range(args.steps)]))
     d_ms = float(np.mean([evs[k][1].elapsed_ms(evs[k][2]) for k in range(args.steps)]))
@@ -374,6 +403,8 @@ def main() -> None:
 
     total_raw = max_over_ranks(raw, op="sum") * args.steps
     value = total_raw / elapsed / GIB
+    per_gpu = gather_ranks(raw * args.steps / mine / GIB)
+    copy_gbs = copy_bandwidth(batch, stream)
     line = {
         "metric": METRIC,
         "value": round(value, 3),
@@ -403,7 +434,9 @@ def main() -> None:
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(dom_ms, 4),
+            "copy_gbs": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 5),
         },
+        "per_gpu_gibs": [round(x, 3) for x in per_gpu],
         "kernels_ms": {"compress": round(c_ms, 4), "decompress": round(d_ms, 4)},
         "compress_gibs": round(raw / (c_ms * 1e-3) / GIB, 2),
         "decompress_gibs": round(raw / (d_ms * 1e-3) / GIB, 2),

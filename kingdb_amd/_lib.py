@@ -67,7 +67,9 @@ SIGNATURES = {
                                   _u64, _vp, _vp]),
     "kdb_hstable_db_options": (_i, [_u64, _u32, _vp]),
     "kdb_hstable_writer_create": (_i, [_u64, _u32, _c.POINTER(_vp)]),
+    "kdb_hstable_writer_create2": (_i, [_u64, _u32, _u32, _c.POINTER(_vp)]),
     "kdb_hstable_writer_append": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
+    "kdb_hstable_writer_append_device": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32]),
     "kdb_hstable_writer_close": (_i, [_vp]),
     "kdb_hstable_writer_file_count": (_i, [_vp, _c.POINTER(_u32)]),
     "kdb_hstable_writer_file": (_i, [_vp, _u32, _c.POINTER(_u32), _c.POINTER(_vp), _c.POINTER(_u64)]),

@@ -27,6 +27,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../include/kdb_put.h"
 
 namespace {
@@ -81,16 +83,34 @@ uint32_t crc32c(const uint8_t* p, size_t n) {
 
 void put32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i)); }
 void put64(uint8_t* p, uint64_t v) { for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i)); }
-size_t varint_len(uint64_t v) {
-  size_t n = 1;
-  while (v >= 128) { v >>= 7; n++; }
-  return n;
-}
 uint8_t* varint(uint8_t* p, uint64_t v) {
   while (v >= 128) { *p++ = (uint8_t)(v | 128); v >>= 7; }
   *p++ = (uint8_t)v;
   return p;
 }
+
+// One varint (up to 10 bytes) with PDEP: the low 56 bits spread over 8 bytes in
+// one instruction, continuation bits or'ed in; always stores 10 bytes (callers
+// keep that much slack) and returns the end of the encoding.
+#if defined(__x86_64__)
+const bool kBmi2 = __builtin_cpu_supports("bmi2");
+inline uint64_t pdep64(uint64_t v, uint64_t mask) {
+  uint64_t r;
+  asm("pdepq %2, %1, %0" : "=r"(r) : "r"(v), "r"(mask));
+  return r;
+}
+inline uint8_t* varint_pdep(uint8_t* p, uint64_t v) {
+  const uint32_t len = (uint32_t)((70 - __builtin_clzll(v | 1)) / 7);      // 1..10
+  uint64_t x = pdep64(v, 0x7f7f7f7f7f7f7f7full);
+  x |= len >= 9 ? 0x8080808080808080ull : 0x8080808080808080ull & ((1ull << (8 * (len - 1))) - 1);
+  memcpy(p, &x, 8);
+  p[8] = (uint8_t)(((v >> 56) & 0x7f) | (len == 10 ? 0x80 : 0));
+  p[9] = 1;
+  return p + len;
+}
+#else
+inline uint8_t* varint_pdep(uint8_t* p, uint64_t v) { return varint(p, v); }
+#endif
 
 // DatabaseOptionEncoder::EncodeTo (format.h:324-340): version 0.9.0.0, data
 // format 1.0, hstable size, hash, compression LZ4 (1), checksum CRC32C (1).
@@ -105,20 +125,60 @@ void db_options(uint64_t hstable_size, uint32_t hash_type, uint8_t* b) {
 }
 
 // A growable byte buffer that does not zero what it is about to overwrite
-// (std::vector::resize would: a second pass over every entry byte).
+// (std::vector::resize would: a second pass over every entry byte).  Pinned
+// buffers (hipHostMalloc) are DMA targets: append_device lands the entry
+// bytes there straight from HBM, with no host copy.
 struct Buf {
-  std::unique_ptr<uint8_t[]> p;
+  uint8_t* p = nullptr;
   size_t cap = 0, n = 0;
-  void reserve(size_t c) {
-    if (c <= cap) return;
-    std::unique_ptr<uint8_t[]> q(new uint8_t[c]);
-    if (n) memcpy(q.get(), p.get(), n);
-    p = std::move(q);
+  bool pinned = false;
+  Buf() = default;
+  explicit Buf(bool pin) : pinned(pin) {}
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  Buf(Buf&& o) noexcept : p(o.p), cap(o.cap), n(o.n), pinned(o.pinned) { o.p = nullptr; o.cap = o.n = 0; }
+  Buf& operator=(Buf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p; cap = o.cap; n = o.n; pinned = o.pinned;
+      o.p = nullptr; o.cap = o.n = 0;
+    }
+    return *this;
+  }
+  ~Buf() { release(); }
+  void release() {
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else delete[] p;
+    }
+    p = nullptr;
+    cap = n = 0;
+  }
+  bool reserve(size_t c) {
+    if (c <= cap) return true;
+    uint8_t* q = nullptr;
+    if (pinned) {
+      if (hipHostMalloc(reinterpret_cast<void**>(&q), c, hipHostMallocDefault) != hipSuccess) return false;
+    } else {
+      q = new uint8_t[c];
+    }
+    if (n) memcpy(q, p, n);
+    const size_t keep = n;
+    release();
+    p = q;
     cap = c;
+    n = keep;
+    return true;
+  }
+  // room for len more bytes (callers with DMA in flight settle it first)
+  uint8_t* grow(size_t len) {
+    if (n + len > cap && !reserve(std::max(n + len, cap * 2))) return nullptr;
+    uint8_t* d = p + n;
+    n += len;
+    return d;
   }
   void append(const void* src, size_t len) {
-    if (n + len > cap) reserve(std::max(n + len, cap * 2));
-    uint8_t* d = p.get() + n;
+    uint8_t* d = grow(len);
     const uint8_t* s = static_cast<const uint8_t*>(src);
     // large runs (a chunk's worth of entries) are copied by a few threads:
     // one core's memcpy is the host side's bottleneck otherwise
@@ -136,11 +196,10 @@ struct Buf {
     } else {
       memcpy(d, s, len);
     }
-    n += len;
   }
   size_t size() const { return n; }
-  uint8_t* data() { return p.get(); }
-  const uint8_t* data() const { return p.get(); }
+  uint8_t* data() { return p; }
+  const uint8_t* data() const { return p; }
 };
 
 }  // namespace
@@ -148,21 +207,38 @@ struct Buf {
 struct kdb_hstable_writer {
   uint64_t size_block;
   uint32_t hash_type;
+  bool pinned = false;                      // file buffers in pinned host memory
+  mutable std::vector<hipStream_t> pending; // streams with entry DMA into the files in flight
   uint32_t fileid = 0;
   uint64_t timestamp = 0;
   bool open = false;
   Buf cur;                                  // the open file's bytes (== offset_end_)
-  std::vector<std::pair<uint64_t, uint32_t>> offarray;
+  Buf rows;                                 // the open file's offset array rows, encoded as appended
+  uint64_t nrows = 0;
   bool padding_flag = false, incomplete = false;
   std::vector<std::pair<uint32_t, Buf>> files;   // closed files
   std::vector<Buf> spare;                   // buffers of files dropped by reset(), reused
 
+  // every entry byte landed (DMA into the file buffers complete)
+  bool settle() const {
+    bool ok = true;
+    for (hipStream_t st : pending) ok &= hipStreamSynchronize(st) == hipSuccess;
+    pending.clear();
+    return ok;
+  }
+  // room for len more bytes of the open file; a reallocation waits for the DMA into the old buffer
+  uint8_t* grow(size_t len) {
+    if (cur.size() + len > cur.cap) settle();
+    return cur.grow(len);
+  }
   void open_file() {                        // OpenNewFile
     fileid++;
     timestamp++;
     if (!spare.empty()) {
       cur = std::move(spare.back());
       spare.pop_back();
+    } else {
+      cur = Buf(pinned);
     }
     cur.reserve(size_block + size_block / 8 * 5 + (1u << 20));   // + offset array (<= 15 B per >= 26 B entry)
     cur.n = 0;
@@ -175,53 +251,27 @@ struct kdb_hstable_writer {
     put64(b + 16, timestamp);
     put32(b, crc32c(b + 4, 20));
     db_options(size_block, hash_type, b + 24);
-    offarray.clear();
-    offarray.reserve(size_block / 64);
+    rows.reserve(std::min<size_t>(size_block / 2, 64u << 20) + 64);
+    rows.n = 0;
+    nrows = 0;
     padding_flag = incomplete = false;
     open = true;
   }
   void close_file() {                       // CloseCurrentFile -> FlushOffsetArray
     if (!open) return;
     if (!incomplete) {
-      // OffsetArrayRow::EncodeTo per entry (varint64 hash, varint32 offset), then the footer
+      // the OffsetArrayRow::EncodeTo rows (varint64 hash, varint32 offset,
+      // encoded as the entries were appended), then the footer
       const size_t start = cur.size();
-      cur.reserve(start + offarray.size() * 15 + 36);
+      if (start + rows.n + 36 > cur.cap) settle();
+      cur.reserve(start + rows.n + 36);
       uint8_t* q = cur.data() + start;
-      const size_t rows = offarray.size();
-      const size_t T = std::min<size_t>(8, rows / 16384 + 1);
-      if (T == 1) {
-        for (auto& r : offarray) {
-          q = varint(q, r.first);
-          q = varint(q, r.second);
-        }
-      } else {                              // rows encoded by T threads into their byte ranges
-        std::vector<size_t> lo(T + 1), bytes(T + 1, 0);
-        for (size_t k = 0; k <= T; k++) lo[k] = rows * k / T;
-        auto each = [&](auto&& fn) {
-          std::vector<std::thread> th;
-          for (size_t k = 1; k < T; k++) th.emplace_back(fn, k);
-          fn(0);
-          for (auto& t : th) t.join();
-        };
-        each([&](size_t k) {
-          size_t b = 0;
-          for (size_t i = lo[k]; i < lo[k + 1]; i++) b += varint_len(offarray[i].first) + varint_len(offarray[i].second);
-          bytes[k + 1] = b;
-        });
-        for (size_t k = 1; k <= T; k++) bytes[k] += bytes[k - 1];
-        each([&](size_t k) {
-          uint8_t* o = q + bytes[k];
-          for (size_t i = lo[k]; i < lo[k + 1]; i++) {
-            o = varint(o, offarray[i].first);
-            o = varint(o, offarray[i].second);
-          }
-        });
-        q += bytes[T];
-      }
+      memcpy(q, rows.data(), rows.n);
+      q += rows.n;
       put32(q, 1);
       put32(q + 4, padding_flag ? 1u : 0u);
       put64(q + 8, start);
-      put64(q + 16, offarray.size());
+      put64(q + 16, nrows);
       put64(q + 24, kMagic);
       q += 32;
       put32(q, crc32c(cur.data() + start, (size_t)(q - (cur.data() + start))));
@@ -241,64 +291,173 @@ int kdb_hstable_db_options(uint64_t hstable_size, uint32_t hash_type, uint8_t* o
   return KDB_PUT_OK;
 }
 
-int kdb_hstable_writer_create(uint64_t hstable_size, uint32_t hash_type, kdb_hstable_writer** w) {
-  if (!w || hash_type > 1 || hstable_size <= kHeaderSize) return KDB_PUT_EINVAL;
-  *w = new kdb_hstable_writer{hstable_size, hash_type};
+int kdb_hstable_writer_create2(uint64_t hstable_size, uint32_t hash_type, uint32_t flags, kdb_hstable_writer** w) {
+  if (!w || hash_type > 1 || hstable_size <= kHeaderSize || (flags & ~KDB_HSTABLE_PINNED)) return KDB_PUT_EINVAL;
+  *w = new kdb_hstable_writer{hstable_size, hash_type, (flags & KDB_HSTABLE_PINNED) != 0};
   return KDB_PUT_OK;
 }
 
-int kdb_hstable_writer_append(kdb_hstable_writer* w, const uint8_t* entries, const uint64_t* entry_off,
-                              const uint32_t* entry_len, const uint64_t* hashed, const uint32_t* kind,
-                              const int32_t* status, uint32_t n) {
-  if (!w || (n && (!entries || !entry_off || !entry_len || !hashed || !kind || !status))) return KDB_PUT_EINVAL;
+int kdb_hstable_writer_create(uint64_t hstable_size, uint32_t hash_type, kdb_hstable_writer** w) {
+  return kdb_hstable_writer_create2(hstable_size, hash_type, 0, w);
+}
+
+}  // extern "C"
+
+namespace {
+
+// WriteOrdersAndFlushFile over one batch; `land(dst, src_off, len)` puts the
+// dense stream's bytes [src_off, src_off+len) at dst (host memcpy, or DMA).
+template <bool kPdep, class Land>
+int append_loop(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t* entry_len, const uint64_t* hashed,
+                const uint32_t* kind, const int32_t* status, uint32_t n, Land land) {
   // Entries are appended in runs: consecutive entries of one file are one
-  // memcpy (the dense stream holds them back to back).
+  // copy (the dense stream holds them back to back).  The open file's row
+  // cursor lives in locals (byte stores would otherwise force reloads of the
+  // writer's fields) and is written back around every call that needs it.
   uint64_t fsize = w->cur.size();           // offset_end_ of the open file, run included
-  const uint8_t* run = nullptr;
-  uint64_t run_len = 0;
-  auto flush_run = [&]() {
-    if (run_len) w->cur.append(run, run_len);
-    run = nullptr;
-    run_len = 0;
+  uint64_t run = 0, run_len = 0;
+  const uint64_t sb = w->size_block;
+  uint8_t* rp = w->rows.data() + w->rows.n;
+  uint8_t* rend = w->rows.data() + (w->rows.cap > 32 ? w->rows.cap - 32 : 0);
+  uint64_t nr = w->nrows;
+  auto sync_rows = [&]() {
+    w->rows.n = (size_t)(rp - w->rows.data());
+    w->nrows = nr;
   };
-  auto close = [&]() {
-    flush_run();
+  auto load_rows = [&]() {
+    rp = w->rows.data() + w->rows.n;
+    rend = w->rows.data() + (w->rows.cap > 32 ? w->rows.cap - 32 : 0);
+    nr = w->nrows;
+  };
+  auto close = [&]() -> int {
+    if (run_len) {
+      const int rc = land(w, run, run_len);
+      run_len = 0;
+      if (rc != KDB_PUT_OK) return rc;
+    }
+    sync_rows();
     w->close_file();
     fsize = 0;
+    return KDB_PUT_OK;
   };
   for (uint32_t i = 0; i < n; i++) {
     if (status[i] != 0) continue;           // the reference returned IOError: no order
-    if (w->open && fsize > w->size_block) close();                    // FlushCurrentFile(true, 0)
+    if (w->open && fsize > sb) {            // FlushCurrentFile(true, 0)
+      const int rc = close();
+      if (rc != KDB_PUT_OK) return rc;
+    }
     if (!w->open) {
       w->open_file();
       fsize = w->cur.size();
+      load_rows();
     }
-    if (fsize > 0xFFFFFFFFull) return KDB_PUT_EINVAL;
-    w->offarray.emplace_back(hashed[i], (uint32_t)fsize);
-    const uint8_t* e = entries + entry_off[i];
-    if (run_len && run + run_len != e) flush_run();
-    if (!run_len) run = e;
+    if (fsize > 0xFFFFFFFFull) {
+      sync_rows();
+      return KDB_PUT_EINVAL;
+    }
+    if (rp > rend) {                        // rows buffer full (tiny entries): grow it
+      sync_rows();
+      w->rows.reserve(w->rows.cap * 2 + 4096);
+      load_rows();
+    }
+    if (kPdep) {
+      rp = varint_pdep(rp, hashed[i]);
+      rp = varint_pdep(rp, fsize);
+    } else {
+      rp = varint(rp, hashed[i]);
+      rp = varint(rp, fsize);
+    }
+    nr++;
+    const uint64_t eo = entry_off[i];
+    if (run_len && run + run_len != eo) {
+      const int rc = land(w, run, run_len);
+      if (rc != KDB_PUT_OK) {
+        sync_rows();
+        return rc;
+      }
+      run_len = 0;
+    }
+    if (!run_len) run = eo;
     run_len += entry_len[i];
     fsize += entry_len[i];
     if (kind[i] != 0) {                     // multipart first part: FlushCurrentFile(0, padding)
       w->padding_flag = true;
       if (kind[i] == 2) w->incomplete = true;
-      if (fsize >= w->size_block) close();
+      if (fsize >= sb) {
+        const int rc = close();
+        if (rc != KDB_PUT_OK) return rc;
+      }
     }
   }
-  flush_run();
-  if (w->open && w->cur.size() >= w->size_block) w->close_file();    // end of batch: FlushCurrentFile(0, 0)
+  if (run_len) {
+    const int rc = land(w, run, run_len);
+    if (rc != KDB_PUT_OK) {
+      sync_rows();
+      return rc;
+    }
+  }
+  sync_rows();
+  if (w->open && w->cur.size() >= sb) w->close_file();    // end of batch: FlushCurrentFile(0, 0)
   return KDB_PUT_OK;
+}
+
+// WriteOrdersAndFlushFile over one batch; `land(w, src_off, len)` puts the
+// dense stream's bytes [src_off, src_off+len) at the end of the open file
+// (host memcpy, or DMA).
+template <class Land>
+int append_batch(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t* entry_len, const uint64_t* hashed,
+                 const uint32_t* kind, const int32_t* status, uint32_t n, Land land) {
+#if defined(__x86_64__)
+  if (kBmi2) return append_loop<true>(w, entry_off, entry_len, hashed, kind, status, n, land);
+#endif
+  return append_loop<false>(w, entry_off, entry_len, hashed, kind, status, n, land);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kdb_hstable_writer_append(kdb_hstable_writer* w, const uint8_t* entries, const uint64_t* entry_off,
+                              const uint32_t* entry_len, const uint64_t* hashed, const uint32_t* kind,
+                              const int32_t* status, uint32_t n) {
+  if (!w || (n && (!entries || !entry_off || !entry_len || !hashed || !kind || !status))) return KDB_PUT_EINVAL;
+  return append_batch(w, entry_off, entry_len, hashed, kind, status, n,
+                      [entries](kdb_hstable_writer* wr, uint64_t off, uint64_t len) {
+                        uint8_t* d = wr->grow(len);
+                        if (!d) return KDB_PUT_EINVAL;
+                        memcpy(d, entries + off, len);
+                        return KDB_PUT_OK;
+                      });
+}
+
+int kdb_hstable_writer_append_device(kdb_hstable_writer* w, void* stream, const uint8_t* d_entries,
+                                     const uint64_t* entry_off, const uint32_t* entry_len, const uint64_t* hashed,
+                                     const uint32_t* kind, const int32_t* status, uint32_t n) {
+  if (!w || (n && (!d_entries || !entry_off || !entry_len || !hashed || !kind || !status))) return KDB_PUT_EINVAL;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  bool used = false;
+  const int rc = append_batch(w, entry_off, entry_len, hashed, kind, status, n,
+                              [&](kdb_hstable_writer* wr, uint64_t off, uint64_t len) {
+                                uint8_t* d = wr->grow(len);
+                                if (!d) return KDB_PUT_EINVAL;
+                                if (hipMemcpyAsync(d, d_entries + off, len, hipMemcpyDeviceToHost, st) != hipSuccess)
+                                  return KDB_PUT_EHIP;
+                                used = true;
+                                return KDB_PUT_OK;
+                              });
+  if (used && std::find(w->pending.begin(), w->pending.end(), st) == w->pending.end()) w->pending.push_back(st);
+  return rc;
 }
 
 int kdb_hstable_writer_close(kdb_hstable_writer* w) {
   if (!w) return KDB_PUT_EINVAL;
   w->close_file();
-  return KDB_PUT_OK;
+  return w->settle() ? KDB_PUT_OK : KDB_PUT_EHIP;
 }
 
 int kdb_hstable_writer_file_count(const kdb_hstable_writer* w, uint32_t* count) {
   if (!w || !count) return KDB_PUT_EINVAL;
+  if (!w->settle()) return KDB_PUT_EHIP;
   *count = (uint32_t)w->files.size();
   return KDB_PUT_OK;
 }
@@ -306,6 +465,7 @@ int kdb_hstable_writer_file_count(const kdb_hstable_writer* w, uint32_t* count) 
 int kdb_hstable_writer_file(const kdb_hstable_writer* w, uint32_t i, uint32_t* fileid, const uint8_t** data,
                             uint64_t* size) {
   if (!w || i >= w->files.size() || !fileid || !data || !size) return KDB_PUT_EINVAL;
+  if (!w->settle()) return KDB_PUT_EHIP;
   *fileid = w->files[i].first;
   *data = w->files[i].second.data();
   *size = w->files[i].second.size();
@@ -314,6 +474,7 @@ int kdb_hstable_writer_file(const kdb_hstable_writer* w, uint32_t i, uint32_t* f
 
 int kdb_hstable_writer_save(const kdb_hstable_writer* w, const char* dir) {
   if (!w || !dir) return KDB_PUT_EINVAL;
+  if (!w->settle()) return KDB_PUT_EHIP;
   for (auto& f : w->files) {
     char name[64];
     snprintf(name, sizeof(name), "/%08x", f.first);      // HSTableManager::GetFilepath
@@ -327,11 +488,13 @@ int kdb_hstable_writer_save(const kdb_hstable_writer* w, const char* dir) {
 
 int kdb_hstable_writer_reset(kdb_hstable_writer* w) {
   if (!w) return KDB_PUT_EINVAL;
+  if (!w->settle()) return KDB_PUT_EHIP;
   for (auto& f : w->files) w->spare.push_back(std::move(f.second));
   w->files.clear();
   if (w->open) w->spare.push_back(std::move(w->cur));
   w->cur = Buf();
-  w->offarray.clear();
+  w->rows.n = 0;
+  w->nrows = 0;
   w->open = w->padding_flag = w->incomplete = false;
   w->fileid = 0;
   w->timestamp = 0;
@@ -339,6 +502,7 @@ int kdb_hstable_writer_reset(kdb_hstable_writer* w) {
 }
 
 int kdb_hstable_writer_destroy(kdb_hstable_writer* w) {
+  if (w) w->settle();
   delete w;
   return KDB_PUT_OK;
 }

@@ -60,11 +60,62 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
   if (osize == 0) return (csize == 1 && (wd.get4(in_off) & 0xffu) == 0) ? 0 : -1;   // lz4.cc:911
   const float lanef = (float)lane;
   int ip = 0, op = 0;
+  // q: the block bytes at ip (only the token and the byte after it are used);
+  // have_q: q was taken from the previous sequence's literal load
+  uint32_t q = 0;
+  bool have_q = false;
 #pragma unroll 1
   for (;;) {
     ip = unii(ip);
     op = unii(op);
-    uint32_t q = wd.get4(in_off + (uint32_t)ip);
+    if (!have_q) q = wd.get4(in_off + (uint32_t)ip);
+    have_q = false;
+    {
+      // Fast path: a sequence that is not the last, with at most one length
+      // byte per run, <= 60 literals and no error.  One 64-lane load of the
+      // literals also yields the offset, the match-length byte and the next
+      // token (v_readlane), instead of scalar window reads.  Anything else --
+      // and every error, so its exact code -- goes through the general path
+      // below from the same token.
+      const uint32_t tk = q & 0xffu, ln = tk >> 4, mn = tk & kMlMask, b1 = (q >> 8) & 0xffu;
+      const int lit = ln == kRunMask ? (int)(kRunMask + b1) : (int)ln;
+      const int ls = ip + 1 + (ln == kRunMask ? 1 : 0);
+      const int opl = op + lit;
+      if ((ln < kRunMask || b1 < 255u) & (lit <= 60) & (opl <= oexit) & (ls + lit <= iend - (int)(2 + 1 + kLastLiterals))) {
+        const uint32_t v = in[ls + (int)lane];
+        const uint32_t e = readlane(v, (uint32_t)lit + 2u);
+        const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
+        const int mlen = (mn == kMlMask ? (int)(kMlMask + e) : (int)mn) + (int)kMinMatch;
+        if ((mn < kMlMask || e < 255u) & (off <= opl) & (opl + mlen <= oend - (int)kLastLiterals)) {
+          out[op + (int)lane] = (uint8_t)v;        // lz4.cc:947 (lanes past lit: not-yet-produced output)
+          const uint32_t nt = (uint32_t)lit + 2u + (mn == kMlMask ? 1u : 0u);   // next token's lane (<= 63)
+          q = readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8);
+          have_q = nt < 63u;
+          ip = ls + lit + 2 + (mn == kMlMask ? 1 : 0);
+          const int ref = opl - off;
+          asm volatile("" ::: "memory");
+          if (off >= mlen || off >= 64) {
+#pragma unroll 1
+            for (int i = 0; i < mlen; i += 64) {
+              const uint8_t b = out[ref + i + (int)lane];
+              out[opl + i + (int)lane] = b;
+              asm volatile("" ::: "memory");
+            }
+          } else if (off > 0) {
+            const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+            const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+#pragma unroll 1
+            for (int i = 0; i < mlen; i += 64) {
+              const uint8_t b = out[ref + i + rr];
+              out[opl + i + (int)lane] = b;
+            }
+          }
+          asm volatile("" ::: "memory");
+          op = opl + mlen;
+          continue;
+        }
+      }
+    }
     const uint32_t token = q & 0xffu;
     ip++;
     int length = (int)(token >> 4);

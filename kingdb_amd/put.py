@@ -160,9 +160,10 @@ def put_entries(puts, hash_type: int = 1, stream: Stream | None = None) -> PutBa
 class HSTableWriter:
     """HSTable files for one database directory (csrc/hstable.cc)."""
 
-    def __init__(self, hstable_size: int = 32 << 20, hash_type: int = 1):
+    def __init__(self, hstable_size: int = 32 << 20, hash_type: int = 1, pinned: bool = False):
         h = ctypes.c_void_p()
-        _lib.check(lib().kdb_hstable_writer_create(hstable_size, hash_type, ctypes.byref(h)), "hstable_writer_create")
+        _lib.check(lib().kdb_hstable_writer_create2(hstable_size, hash_type, 1 if pinned else 0, ctypes.byref(h)),
+                   "hstable_writer_create")
         self.h = h.value
         self.hstable_size, self.hash_type = hstable_size, hash_type
 
@@ -178,6 +179,14 @@ class HSTableWriter:
         """append() from host pointers (pinned buffers of the bench pipeline)."""
         _lib.check(lib().kdb_hstable_writer_append(self.h, entries_ptr, entry_off_ptr, entry_len_ptr, hashed_ptr,
                                                    kind_ptr, status_ptr, n), "hstable_writer_append")
+
+    def append_device(self, stream_ptr: int, d_entries: int, entry_off_ptr: int, entry_len_ptr: int,
+                      hashed_ptr: int, kind_ptr: int, status_ptr: int, n: int) -> None:
+        """append() with the entry bytes still on the device: DMA on `stream`
+        straight into the files (host pointers for the per-entry arrays)."""
+        _lib.check(lib().kdb_hstable_writer_append_device(self.h, stream_ptr, d_entries, entry_off_ptr, entry_len_ptr,
+                                                          hashed_ptr, kind_ptr, status_ptr, n),
+                   "hstable_writer_append_device")
 
     def close(self) -> None:
         _lib.check(lib().kdb_hstable_writer_close(self.h), "hstable_writer_close")

@@ -8,13 +8,15 @@ and writes them in batches.  Here a batch of puts is the unit: per chunk of
 `chunk` puts, over `nstreams` HIP streams,
 
   H2D keys + values + metadata -> kdb_put_entries_batch (frame policy, LZ4,
-  CRC32C, key hash, EntryHeader: csrc/put.hip) -> D2H of the chunk's entry
-  bytes (exactly Σ entry_len) + per-entry hash/kind/status
-  -> host HSTable framing (csrc/hstable.cc), in put order
+  CRC32C, key hash, EntryHeader: csrc/put.hip) -> D2H of the per-entry
+  offset/length/hash/kind/status -> host HSTable framing (csrc/hstable.cc),
+  in put order, which DMAs the entry bytes (exactly Σ entry_len) from HBM
+  straight into the pinned file buffers (direct=True; direct=False lands them
+  in a pinned staging buffer and memcpys them into the files)
 
 with the copies and kernels of later chunks overlapping the host framing of
 earlier ones.  Timing is host wall clock from the first enqueue to the last
-entry framed.  Nothing here computes on the CPU except that framing.
+entry byte in its file.  Nothing here computes on the CPU except that framing.
 """
 from __future__ import annotations
 
@@ -32,11 +34,11 @@ class PutPipeline:
     """n puts of fixed-size keys and values (the db_bench shape)."""
 
     def __init__(self, n: int, key_size: int, value_size: int, chunk: int = 1 << 16, nstreams: int = 4,
-                 hstable_size: int = 32 << 20, hash_type: int = 1):
+                 hstable_size: int = 32 << 20, hash_type: int = 1, direct: bool = True):
         self.n, self.ks, self.vs = int(n), int(key_size), int(value_size)
         self.chunk = max(1, min(int(chunk), self.n))
         self.nchunks = (self.n + self.chunk - 1) // self.chunk
-        self.hstable_size, self.hash_type = hstable_size, hash_type
+        self.hstable_size, self.hash_type, self.direct = hstable_size, hash_type, bool(direct)
         self.streams = [Stream() for _ in range(max(1, nstreams))]
         n, c = self.n, self.chunk
         self.h_keys = PinnedBuffer(n * self.ks)
@@ -58,7 +60,7 @@ class PutPipeline:
             b.vmeta.upload(self.meta)
             b.chunks.upload(self.h_chunks.np)
         # per stream slot: pinned landing zones for one chunk's outputs
-        self.h_ent = [PinnedBuffer(b.entries_cap) for b in self.batches]
+        self.h_ent = [] if self.direct else [PinnedBuffer(b.entries_cap) for b in self.batches]
         self.h_out = [PinnedBuffer(32 * c + 64) for _ in self.batches]
         self.writer: HSTableWriter | None = None
 
@@ -71,7 +73,7 @@ class PutPipeline:
         L = lib()
         S = len(self.streams)
         if self.writer is None:
-            self.writer = HSTableWriter(self.hstable_size, self.hash_type)
+            self.writer = HSTableWriter(self.hstable_size, self.hash_type, pinned=self.direct)
         else:
             self.writer.reset()     # a fresh directory; file buffers (like buffer_raw_) are reused
         w = self.writer
@@ -86,13 +88,17 @@ class PutPipeline:
             ta = time.perf_counter()
             _lib.check(L.kdb_lz4_event_sync(tot_ev[k].ptr), "event_sync")
             ho = self.h_out[s]
-            total = int(ho.np[32 * m:32 * m + 8].view(np.uint64)[0])
-            if total:
-                _lib.check(L.kdb_lz4_memcpy_d2h(self.h_ent[s].ptr, b.entries.ptr, total, st.ptr), "d2h entries")
-            st.sync()
-            tb = time.perf_counter()
             p = ho.ptr
-            w.append_raw(self.h_ent[s].ptr, p, p + 8 * m, p + 12 * m, p + 24 * m, p + 28 * m, m)
+            if self.direct:
+                tb = time.perf_counter()
+                w.append_device(st.ptr, b.entries.ptr, p, p + 8 * m, p + 12 * m, p + 24 * m, p + 28 * m, m)
+            else:
+                total = int(ho.np[32 * m:32 * m + 8].view(np.uint64)[0])
+                if total:
+                    _lib.check(L.kdb_lz4_memcpy_d2h(self.h_ent[s].ptr, b.entries.ptr, total, st.ptr), "d2h entries")
+                st.sync()
+                tb = time.perf_counter()
+                w.append_raw(self.h_ent[s].ptr, p, p + 8 * m, p + 12 * m, p + 24 * m, p + 28 * m, m)
             self.stats["wait_s"] += tb - ta
             self.stats["frame_s"] += time.perf_counter() - tb
 
@@ -116,7 +122,7 @@ class PutPipeline:
                 drain(k - (S - 1))
         for k in range(max(0, self.nchunks - (S - 1)), self.nchunks):
             drain(k)
-        w.close()
+        w.close()                   # + every entry byte landed
         return time.perf_counter() - t0
 
     def free(self) -> None:

@@ -81,3 +81,14 @@ def max_over_ranks(seconds: float, op: str = "max") -> float:
     t = torch.tensor([float(seconds)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.SUM if op == "sum" else dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_ranks(x: float) -> list[float]:
+    """A scalar from every rank, in rank order (the bench's per-GPU rates);
+    [x] when torch.distributed is not initialised."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(x)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, float(x))
+    return [float(v) for v in out]

@@ -59,6 +59,36 @@ def test_malformed_return_codes(gpu):
             assert out == g["out"][o:o + r].tobytes(), i
 
 
+def test_decompress_mutants_vs_oracle(gpu, orc):
+    """Return codes and outputs of mutated, truncated and undersized blocks equal
+    the oracle's (pinned to the reference by malformed.npz): every error must be
+    caught at the same input position whichever decoder path a sequence takes."""
+    rng = random.Random(77)
+    pool = oracle.g1_pool(orc)
+    vals = oracle.g1_values(pool, 4096, 12) + oracle.g1_values(pool, 100, 12)
+    for _ in range(24):
+        n = rng.choice([20, 300, 2000, 4096, 8000])
+        p = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 90)))
+        vals.append((p * (n // len(p) + 1))[:n])
+    blocks, sizes = [], []
+    for v in vals:
+        b = orc.compress(v)
+        for k in range(8):
+            m = bytearray(b)
+            for _ in range(rng.randrange(1, 4)):
+                m[rng.randrange(len(m))] = rng.randrange(256)
+            blocks.append(bytes(m))
+            sizes.append(len(v))
+        blocks += [b[:rng.randrange(1, len(b))], b, b, b]
+        sizes += [len(v), max(len(v) - rng.randrange(1, 20), 0), len(v) + 7, max(len(v) - 1, 0)]
+    got = gpu.decompress_blocks(blocks, sizes)
+    for i, ((r, out), b, s) in enumerate(zip(got, blocks, sizes)):
+        er, eout = orc.decompress(b, s)
+        assert r == er, (i, r, er)
+        if r > 0:
+            assert out == eout, i
+
+
 def test_g1_db_bench_values(gpu, orc):
     """db_bench G1 values (SURVEY KATs T3-T5) compressed in one launch per size."""
     g = load_golden("g1_db_bench.npz")

@@ -10,7 +10,7 @@ import socket
 import numpy as np
 import pytest
 
-from kingdb_amd.shard import byte_balanced_ranges, g1_first_piece, max_over_ranks, stitch_offsets
+from kingdb_amd.shard import byte_balanced_ranges, g1_first_piece, gather_ranks, max_over_ranks, stitch_offsets
 
 
 def test_ranges_cover_and_balance():
@@ -50,6 +50,7 @@ def test_edge_cases():
     assert g1_first_piece(0, 1 << 20, 4096) == 0
     assert g1_first_piece(3, 1000, 4096) == 3 * 40960
     assert max_over_ranks(1.5) == 1.5  # no process group
+    assert gather_ranks(2.5) == [2.5]
 
 
 def _free_port():
@@ -76,6 +77,8 @@ def _worker(rank, world, port, out_dir):
     dist.all_gather_object(totals, len(mine))
     off = int(stitch_offsets(totals)[rank])
     elapsed = max_over_ranks(0.25 * (rank + 1))
+    assert gather_ranks(10.0 + rank) == [10.0 + r for r in range(world)]
+    assert max_over_ranks(float(hi - lo), op="sum") == len(values)
     with open(os.path.join(out_dir, f"rank{rank}.bin"), "wb") as f:
         f.write(mine)
     with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:

@@ -182,3 +182,38 @@ def test_gpu_crc_and_hash_random(gpu, orc):
             pv = orc.put_value(k, v)
             assert int(r.crc[i]) == pv["crc"], i
             assert int(r.hashed[i]) == (xxhash.xxh64_intdigest(k) if ht else orc.murmur3_64(k)), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direct", [True, False])
+def test_gpu_put_pipeline_matches_oracle(gpu, orc, direct):
+    """The bench's pipeline (kingdb_amd/putpipe.py: chunks over 4 streams, entry
+    bytes DMA'd from HBM straight into pinned file buffers when direct) writes
+    the oracle's files; small HSTables so files roll over inside and across
+    chunks, and twice through one writer (reset + buffer reuse)."""
+    import oracle
+    from oracle import hstable
+    from kingdb_amd.putpipe import PutPipeline
+    n, ks, vs, hs = 6000, 16, 100, 96 << 10
+    pool = oracle.g1_pool(orc)
+    vals = oracle.g1_values(pool, vs, n)
+    keys = [b"%016d" % i for i in range(n)]
+    w = hstable.Writer(orc, hs, 1)
+    chunk = 1024
+    for lo in range(0, n, chunk):                 # one write-buffer flush per pipeline chunk
+        for k, v in zip(keys[lo:lo + chunk], vals[lo:lo + chunk]):
+            w.put(k, v, None)
+        w._flush(0, 0)
+    exp = w.close()
+    pp = PutPipeline(n, ks, vs, chunk=chunk, nstreams=4, hstable_size=hs, hash_type=1, direct=direct)
+    try:
+        pp.h_keys.np[:] = np.frombuffer(b"".join(keys), np.uint8)
+        pp.h_vals.np[:] = np.frombuffer(b"".join(vals), np.uint8)
+        for _ in range(2):
+            pp.run()
+            got = pp.writer.files()
+            assert list(got) == list(exp)
+            for f in exp:
+                assert got[f] == exp[f], f
+    finally:
+        pp.free()
