@@ -63,13 +63,13 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
   // q: the block bytes at ip (only the token and the byte after it are used);
   // have_q: q was taken from the previous sequence's literal load
   uint32_t q = 0;
-  bool have_q = false;
+  int have_q = 0;
 #pragma unroll 1
   for (;;) {
     ip = unii(ip);
     op = unii(op);
-    if (!have_q) q = wd.get4(in_off + (uint32_t)ip);
-    have_q = false;
+    if (have_q == 0) q = wd.get4(in_off + (uint32_t)ip);
+    have_q = 0;
     {
       // Fast path: a sequence that is not the last, with at most one length
       // byte per run, <= 60 literals and no error.  One 64-lane load of the
@@ -77,37 +77,48 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // token (v_readlane), instead of scalar window reads.  Anything else --
       // and every error, so its exact code -- goes through the general path
       // below from the same token.
-      const uint32_t tk = q & 0xffu, ln = tk >> 4, mn = tk & kMlMask, b1 = (q >> 8) & 0xffu;
-      const int lit = ln == kRunMask ? (int)(kRunMask + b1) : (int)ln;
-      const int ls = ip + 1 + (ln == kRunMask ? 1 : 0);
+      // (conditions as sign bits of plain integers: one scalar compare each,
+      // instead of a chain of 64-bit lane-mask selects)
+      const int tk = (int)(q & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((q >> 8) & 0xffu);
+      const int lx = (ln + 1) >> 4;                               // a literal-length byte follows
+      const int lit = ln + (lx ? b1 : 0);
+      const int ls = ip + 1 + lx;
       const int opl = op + lit;
-      if ((ln < kRunMask || b1 < 255u) & (lit <= 60) & (opl <= oexit) & (ls + lit <= iend - (int)(2 + 1 + kLastLiterals))) {
+      // ok: (ln < 15 || b1 < 255); bad: lit > 60 || opl > oexit || not-last fails
+      const int ok1 = (ln - (int)kRunMask) | (b1 - 255);
+      const int bad1 = (60 - lit) | (oexit - opl) | (iend - (int)(2 + 1 + kLastLiterals) - ls - lit);
+      if ((ok1 & ~bad1) < 0) {
         const uint32_t v = in[ls + (int)lane];
-        const uint32_t e = readlane(v, (uint32_t)lit + 2u);
+        const int e = (int)readlane(v, (uint32_t)lit + 2u);
         const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
-        const int mlen = (mn == kMlMask ? (int)(kMlMask + e) : (int)mn) + (int)kMinMatch;
-        if ((mn < kMlMask || e < 255u) & (off <= opl) & (opl + mlen <= oend - (int)kLastLiterals)) {
+        const int mx = (mn + 1) >> 4;                             // a match-length byte follows
+        const int mlen = mn + (mx ? e : 0) + (int)kMinMatch;
+        const int ok2 = (mn - (int)kMlMask) | (e - 255);
+        const int bad2 = (opl - off) | (oend - (int)kLastLiterals - opl - mlen);
+        if ((ok2 & ~bad2) < 0) {
           out[op + (int)lane] = (uint8_t)v;        // lz4.cc:947 (lanes past lit: not-yet-produced output)
-          const uint32_t nt = (uint32_t)lit + 2u + (mn == kMlMask ? 1u : 0u);   // next token's lane (<= 63)
+          const uint32_t nt = (uint32_t)(lit + 2 + mx);             // next token's lane (<= 63)
           q = readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8);
-          have_q = nt < 63u;
-          ip = ls + lit + 2 + (mn == kMlMask ? 1 : 0);
+          have_q = (int)(63u - nt);             // > 0: the byte after the token was in the load too
+          ip = ls + lit + 2 + mx;
           const int ref = opl - off;
           asm volatile("" ::: "memory");
-          if (off >= mlen || off >= 64) {
+          if (off < min(mlen, 64)) {
+            if (off > 0) {                          // periodic (see the general path)
+              const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+              const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+#pragma unroll 1
+              for (int i = 0; i < mlen; i += 64) {
+                const uint8_t b = out[ref + i + rr];
+                out[opl + i + (int)lane] = b;
+              }
+            }
+          } else {
 #pragma unroll 1
             for (int i = 0; i < mlen; i += 64) {
               const uint8_t b = out[ref + i + (int)lane];
               out[opl + i + (int)lane] = b;
               asm volatile("" ::: "memory");
-            }
-          } else if (off > 0) {
-            const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-            const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
-#pragma unroll 1
-            for (int i = 0; i < mlen; i += 64) {
-              const uint8_t b = out[ref + i + rr];
-              out[opl + i + (int)lane] = b;
             }
           }
           asm volatile("" ::: "memory");
@@ -362,12 +373,84 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
   if (osize == 0) return (csize == 1 && (wd.get4(0) & 0xffu) == 0) ? 0 : -1;   // lz4.cc:911
   const float lanef = (float)lane;
   int ip = 0, op = 0;
+  uint32_t q = 0;
+  int have_q = 0;                          // as in decode_block
 #pragma unroll 1
   for (;;) {
     ip = unii(ip);
     op = unii(op);
     if (in.ensure((uint32_t)ip + kIMirror)) wd.invalidate();
-    uint32_t q = wd.get4((uint32_t)ip);
+    if (have_q == 0) q = wd.get4((uint32_t)ip);
+    have_q = 0;
+    {
+      // decode_block's fast path, over the rings: the literal load reads the
+      // input ring (its mirror covers the wrap; ensure() staged 512 bytes past
+      // ip), stores are masked (ring slots past the run may still be match
+      // sources), and the match source must lie in the output ring.
+      const int tk = (int)(q & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((q >> 8) & 0xffu);
+      const int lx = (ln + 1) >> 4;
+      const int lit = ln + (lx ? b1 : 0);
+      const int ls = ip + 1 + lx;
+      const int opl = op + lit;
+      const int ok1 = (ln - (int)kRunMask) | (b1 - 255);
+      const int bad1 = (60 - lit) | (oexit - opl) | (iend - (int)(2 + 1 + kLastLiterals) - ls - lit);
+      if ((ok1 & ~bad1) < 0) {
+        const uint32_t v = in.lds[((uint32_t)ls & kIMask) + lane];
+        const int e = (int)readlane(v, (uint32_t)lit + 2u);
+        const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
+        const int mx = (mn + 1) >> 4;
+        const int mlen = mn + (mx ? e : 0) + (int)kMinMatch;
+        const int ok2 = (mn - (int)kMlMask) | (e - 255);
+        const int bad2 = (opl - off) | (oend - (int)kLastLiterals - opl - mlen) | ((int)kORing - off);
+        if ((ok2 & ~bad2) < 0) {
+          if ((int)lane < lit) {
+            ring[(uint32_t)(op + (int)lane) & kOMask] = (uint8_t)v;
+            o[op + (int)lane] = (uint8_t)v;
+          }
+          const uint32_t nt = (uint32_t)(lit + 2 + mx);
+          q = readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8);
+          have_q = (int)(63u - nt);
+          ip = ls + lit + 2 + mx;
+          const int ref = opl - off;
+          asm volatile("" ::: "memory");
+          if (off < min(mlen, 64)) {
+            if (off > 0) {
+              const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+              const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+#pragma unroll 1
+              for (int i = 0; i < mlen; i += 64) {
+                const int j = i + (int)lane;
+                const uint8_t b = ring[(uint32_t)(ref + i + rr) & kOMask];
+                if (j < mlen) {
+                  ring[(uint32_t)(opl + j) & kOMask] = b;
+                  o[opl + j] = b;
+                }
+              }
+            } else {
+#pragma unroll 1
+              for (int i = 0; i < mlen; i += 64) {
+                const int j = i + (int)lane;
+                if (j < mlen) o[opl + j] = ring[(uint32_t)(opl + j) & kOMask];
+              }
+            }
+          } else {
+#pragma unroll 1
+            for (int i = 0; i < mlen; i += 64) {
+              const int j = i + (int)lane;
+              const uint8_t b = ring[(uint32_t)(ref + j) & kOMask];
+              if (j < mlen) {
+                ring[(uint32_t)(opl + j) & kOMask] = b;
+                o[opl + j] = b;
+              }
+              asm volatile("" ::: "memory");
+            }
+          }
+          asm volatile("" ::: "memory");
+          op = opl + mlen;
+          continue;
+        }
+      }
+    }
     const uint32_t token = q & 0xffu;
     ip++;
     int length = (int)(token >> 4);

@@ -65,9 +65,9 @@ def test_decompress_mutants_vs_oracle(gpu, orc):
     caught at the same input position whichever decoder path a sequence takes."""
     rng = random.Random(77)
     pool = oracle.g1_pool(orc)
-    vals = oracle.g1_values(pool, 4096, 12) + oracle.g1_values(pool, 100, 12)
+    vals = oracle.g1_values(pool, 4096, 12) + oracle.g1_values(pool, 100, 12) + oracle.g1_values(pool, 65536, 4)
     for _ in range(24):
-        n = rng.choice([20, 300, 2000, 4096, 8000])
+        n = rng.choice([20, 300, 2000, 4096, 8000, 30000, 70000])   # > 8 KiB: the ring decoder
         p = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 90)))
         vals.append((p * (n // len(p) + 1))[:n])
     blocks, sizes = [], []
