@@ -73,6 +73,51 @@ uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
   return (uint32_t)(n < slots ? n : slots);
 }
 
+// Fork/join of a second stream, so that size-class launches overlap: the
+// long-latency big-value class runs beside the small classes, and its tail
+// (the last few big values) no longer idles the rest of the GPU.  One
+// non-blocking stream and two events per host thread and device.
+namespace {
+struct Fork {
+  hipStream_t aux = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+thread_local std::unordered_map<int, Fork> t_fork;
+}  // namespace
+
+hipError_t fork_begin(hipStream_t st, hipStream_t* aux) {
+  static const bool off = [] {
+    const char* e = getenv("KDB_LZ4_NOFORK");     // diagnostic: classes in sequence on one stream
+    return e && *e && *e != '0';
+  }();
+  *aux = st;
+  if (off) return hipSuccess;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  Fork& f = t_fork[dev];
+  if (!f.aux) {
+    if ((e = hipStreamCreateWithFlags(&f.aux, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&f.join, hipEventDisableTiming)) != hipSuccess) return e;
+  }
+  if ((e = hipEventRecord(f.fork, st)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(f.aux, f.fork, 0)) != hipSuccess) return e;
+  *aux = f.aux;
+  return hipSuccess;
+}
+
+// st waits for everything queued on aux (no-op when aux == st)
+hipError_t fork_end(hipStream_t st, hipStream_t aux) {
+  if (aux == st) return hipSuccess;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  Fork& f = t_fork[dev];
+  if ((e = hipEventRecord(f.join, aux)) != hipSuccess) return e;
+  return hipStreamWaitEvent(st, f.join, 0);
+}
+
 // Values per counter claim: ~1/8 of a workgroup's share, at most 16, so the
 // claim rate stays far below one counter's ceiling and the tail stays short.
 uint32_t claim_batch(uint32_t n, uint32_t grid) {

@@ -110,6 +110,7 @@ struct LdsSrc {
   const uint8_t* p;
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
   __device__ __forceinline__ uint32_t rd32(uint32_t i) const { return lds_rd32(p, i); }
+  __device__ __forceinline__ uint32_t prefetch(uint32_t, uint32_t, uint32_t) const { return 0u; }
 };
 
 // Value bytes read in place from global memory (any alignment).  An aligned
@@ -121,6 +122,30 @@ struct GlobalSrc {
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3u);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(g + i - mis);
     return __builtin_amdgcn_alignbyte(w[mis ? 1 : 0], w[0], mis);
+  }
+  // Touches the 256 bytes from p + 256 (one aligned dword per lane, clamped
+  // into the value) so the search frontier is in L1/L2 before it is parsed;
+  // `keep` is the previous call's dword, consumed here -- one sequence later,
+  // when it has long arrived -- so the compiler keeps the load.
+#ifndef KDB_PF_AHEAD
+#define KDB_PF_AHEAD 256u
+#endif
+#ifndef KDB_PF_DW
+#define KDB_PF_DW 1u
+#endif
+  __device__ __forceinline__ uint32_t prefetch(uint32_t p, uint32_t S, uint32_t keep) const {
+#ifdef KDB_PF_OFF
+    return 0u;
+#else
+    asm volatile("" ::"v"(keep));
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < KDB_PF_DW; ++k) {
+      const uint32_t a = min(p + KDB_PF_AHEAD + 256u * k + 4u * lane_id(), S - 1u);
+      x ^= *reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(g + a) & ~(uintptr_t)3);
+    }
+    return x;
+#endif
   }
 };
 
@@ -205,7 +230,9 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
     // _next_match: no catch-up, no literals.
     uint32_t s = 1;                                         // lz4.cc:487
     uint32_t t0 = 0;                                        // 1: lane 0 of the first chunk is the test
+    uint32_t pf = 0;                                        // GlobalSrc: the frontier prefetch in flight
     for (;;) {
+      pf = src.prefetch(s, S, pf);
       // ================= search (lz4.cc:494-527), 64 iterations per step
       uint32_t ip = 0, ref = 0;
       bool found = false, catchup = true;
@@ -690,6 +717,35 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     hipLaunchKernelGGL(class_census_kernel, dim3(min((n + 255u) / 256u, 1024u)), dim3(256), 0, st, src_len, n,
                        kSmallMax, b1, k64KLimit - 1u, census);
   }
+  // The in-place classes (8 KiB .. 65 546 B, and byU32) go first, on a
+  // forked stream: their values take longest, and the small classes fill the
+  // GPU around their tail.
+  static const uint32_t mid_split = [] {
+    const char* e = getenv("KDB_LZ4_CSPLIT");
+    return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : kMidLdsMax;
+  }();
+  const uint32_t glo = max(mid_split, kSmallMax) + 1u;
+  const bool in_place = max_len >= glo;
+  hipStream_t aux = st;
+  if (in_place) {
+    e = fork_begin(st, &aux);
+    if (e != hipSuccess) return e;
+  }
+  if (max_len >= glo && glo < k64KLimit) {
+    const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
+    e = frame ? launch_big<true, false>(aux, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
+                                        ret, census, 2)
+              : launch_big<false, false>(aux, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
+                                         ret, census, 2);
+    if (e != hipSuccess) return e;
+  }
+  if (max_len >= k64KLimit) {
+    e = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
+                                       frame_len, ret, census, 3)
+              : launch_big<false, true>(aux, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
+                                        frame_len, ret, census, 3);
+    if (e != hipSuccess) return e;
+  }
   {
     size_t lds = compress_lds_bytes(kSmallMax);
 #ifdef KDB_ABL_OCC
@@ -704,10 +760,6 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
   // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
   // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
-  static const uint32_t mid_split = [] {
-    const char* e = getenv("KDB_LZ4_CSPLIT");
-    return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : kMidLdsMax;
-  }();
   if (max_len > kSmallMax && mid_split > kSmallMax) {
     const uint32_t hi = min(min(max_len, mid_split), k64KLimit - 1u);
     const size_t lds = compress_lds_bytes(hi);
@@ -717,21 +769,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                                          dst_cap, frame_len, ret, census, 1);
     if (e != hipSuccess) return e;
   }
-  const uint32_t glo = max(mid_split, kSmallMax) + 1u;
-  if (max_len >= glo && glo < k64KLimit) {
-    const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
-    e = frame ? launch_big<true, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len, ret,
-                                        census, 2)
-              : launch_big<false, false>(st, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
-                                         ret, census, 2);
-    if (e != hipSuccess) return e;
-  }
-  if (max_len >= k64KLimit)
-    e = frame ? launch_big<true, true>(st, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
-                                       frame_len, ret, census, 3)
-              : launch_big<false, true>(st, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
-                                        frame_len, ret, census, 3);
-  return e;
+  return fork_end(st, aux);
 }
 
 }  // namespace kdb_lz4

@@ -265,8 +265,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
       tgt = target ? (int)uni(target[v]) : osize;
     }
     if ((uint32_t)csize > in_cap || (uint32_t)osize > out_cap_max || csize < 0 || osize < 0) {
-      // values too large for this launch's LDS: the ring decoder's (launched
-      // after it on the same stream) when skip_big, else unsupported
+      // values too large for this launch's LDS: the ring decoder's (its own
+      // launch, beside this one) when skip_big, else unsupported
       if (skip_big && csize >= 0 && osize >= 0) continue;
       if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
       continue;
@@ -745,13 +745,22 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
   const uint32_t mi = max_in < in_split ? max_in : in_split;
   const uint32_t mo = max_out < split ? max_out : split;
   const size_t lds = decompress_lds_bytes(mi, mo);
-  hipError_t e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
-                                          out_len, ret, big ? 1u : 0u)
-                       : launch_one<false>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
-                                           out_len, ret, big ? 1u : 0u);
-  if (e != hipSuccess || !big) return e;
-  return frame ? launch_ring<true>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
-               : launch_ring<false>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
+  // the ring decoder's class first, on a forked stream (its values take
+  // longest); the two launches write disjoint values
+  hipStream_t aux = st;
+  hipError_t e = hipSuccess;
+  if (big) {
+    if ((e = fork_begin(st, &aux)) != hipSuccess) return e;
+    e = frame ? launch_ring<true>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
+              : launch_ring<false>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
+    if (e != hipSuccess) return e;
+  }
+  e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
+                               out_len, ret, big ? 1u : 0u)
+            : launch_one<false>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
+                                out_len, ret, big ? 1u : 0u);
+  if (e != hipSuccess) return e;
+  return fork_end(st, aux);
 }
 
 }  // namespace kdb_lz4

@@ -132,5 +132,9 @@ __device__ __forceinline__ void flush_lds_to_global(uint8_t* g, const uint8_t* l
 hipError_t work_counter(hipStream_t st, uint32_t** ctr);
 uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
 uint32_t claim_batch(uint32_t n, uint32_t grid);
+// size-class launches on a second stream: *aux waits for st's work so far;
+// fork_end makes st wait for aux (KDB_LZ4_NOFORK=1: aux == st)
+hipError_t fork_begin(hipStream_t st, hipStream_t* aux);
+hipError_t fork_end(hipStream_t st, hipStream_t aux);
 
 }  // namespace kdb_lz4
