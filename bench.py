@@ -43,11 +43,12 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--values", type=int, default=1 << 20, help="values per GPU")
     p.add_argument("--size", type=int, default=4096, help="bytes per value")
-    p.add_argument("--workload", choices=("uniform", "mixed", "put"), default="uniform",
+    p.add_argument("--workload", choices=("uniform", "mixed", "put", "get"), default="uniform",
                    help="uniform: --values x --size (configs[2], the headline); mixed: configs[3], "
                         "--values per GPU of 90%% 100 B / 9%% 4 KiB / 1%% 64 KiB parts, byte-balanced shards; "
                         "put: configs[4], --values puts per GPU of 16 B keys / 100 B values from pinned host "
-                        "memory to HSTable file bytes in host memory")
+                        "memory to HSTable file bytes in host memory; get: the read path (configs[1] shape), "
+                        "UncompressByteArray over --values stored --size B values resident in HBM")
     p.add_argument("--put-host-copy", action="store_true",
                    help="put workload: land entry bytes in a pinned staging buffer and memcpy them into the "
                         "files (the default DMAs them from HBM straight into pinned file buffers)")
@@ -217,6 +218,138 @@ def ref_write_path(keys: np.ndarray, vals: np.ndarray) -> dict | None:
                       "compiled from the reference (oracle/_ref/ref_db)"}
 
 
+def ref_read_path(stored: np.ndarray, off: np.ndarray, lens: np.ndarray, size: int, seconds: float) -> dict | None:
+    """configs[1] CPU path: the reference's CompressorLZ4::UncompressByteArray
+    (oracle/_ref, compiled from /root/reference) over a bounded sample of the
+    same stored values, on all host cores; None where not built."""
+    import oracle  # checker / baseline only
+    if not os.path.exists(oracle.REF_SO):
+        return None
+    lib = ctypes.CDLL(oracle.REF_SO)
+    fn = lib.ref_bench_get
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
+                   ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    n = len(lens)
+    off = np.ascontiguousarray(off, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint64)
+    t = ctypes.c_double()
+    if fn(stored.ctypes.data, off.ctypes.data, lens.ctypes.data, n, size, threads, 1, ctypes.byref(t)) != 0:
+        raise RuntimeError("reference read path failed on the sample")
+    passes = int(min(50, max(1, math.ceil(seconds / max(t.value, 1e-3)))))
+    if fn(stored.ctypes.data, off.ctypes.data, lens.ctypes.data, n, size, threads, passes, ctypes.byref(t)) != 0:
+        raise RuntimeError("reference read path failed on the sample")
+    return {"value": round(float(n) * size * passes / t.value / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"{n} stored {size} B G1-long values (the first of the GPU batch), {passes} timed passes after "
+                      f"1 warm-up, blocked over {threads} threads; CPU: {cpu_model()}",
+            "source": "algorithm/compressor.cc CompressorLZ4::UncompressByteArray (verify off), compiled from the "
+                      "reference (oracle/_ref)"}
+
+
+def bench_get(args, world: int, rank: int, local: int, barrier, sync_all) -> None:
+    """configs[1] as KingDB reads it: Database::GetRaw's UncompressByteArray over
+    a batch of stored values (one frame each at 4 KiB) already in HBM -- the
+    frame walk, the frame decode and the status/size pass of
+    kdb_get_values_batch (csrc/get.hip), verify off (ReadOptions' default)."""
+    import kingdb_amd as K
+    from kingdb_amd import _lib
+    from kingdb_amd import lz4 as L
+    from kingdb_amd.lz4 import DeviceBuffer
+    from kingdb_amd.shard import g1_first_piece, gather_ranks, max_over_ranks
+    n, size = args.values, args.size
+    stream = K.Stream()
+    batch = K.DeviceBatch.g1_long(n, size, first_piece=g1_first_piece(rank, n, size), stream=stream)
+    batch.compress(stream)            # the stored values: one CompressorLZ4 frame each
+    stream.sync()
+    cst, _ = batch.status()
+    if not (cst == 0).all():
+        raise SystemExit("bench: could not build the stored values")
+    flen = batch.frame_lens().astype(np.uint64)
+    sizes = batch.sizes.astype(np.uint64)
+    zeros32 = np.zeros(n, np.uint32)
+    # stored_off u64 | avail u64 | svc u64 | size u64 | out_off u64 | checksum u32 | checksum_initial u32 |
+    # out_len u64 | status i32
+    m = np.concatenate([batch.frame_off.astype(np.uint64).view(np.uint8), flen.view(np.uint8), flen.view(np.uint8),
+                        sizes.view(np.uint8), batch.src_off.astype(np.uint64).view(np.uint8), zeros32.view(np.uint8),
+                        zeros32.view(np.uint8), np.zeros(n, np.uint64).view(np.uint8), np.zeros(n, np.int32).view(np.uint8)])
+    meta = DeviceBuffer(m.nbytes)
+    meta.upload(m, stream=stream.ptr)
+    lib = L.lib()
+    frame_cap = n
+    sb = int(lib.kdb_get_scratch_bytes(n, frame_cap))
+    scratch = DeviceBuffer(sb)
+    b = meta.ptr
+    max_in = int(flen.max())
+
+    def step():
+        _lib.check(lib.kdb_get_values_batch(stream.ptr, batch.frames.ptr, b, b + 8 * n, b + 16 * n, b + 24 * n, n,
+                                            batch.out.ptr, b + 32 * n, 0, b + 40 * n, b + 44 * n, frame_cap, max_in,
+                                            size, scratch.ptr, sb, b + 48 * n, b + 56 * n), "kdb_get_values_batch")
+    for _ in range(args.warmup):
+        step()
+    stream.sync()
+    evs = [(K.Event(), K.Event()) for _ in range(args.steps)]
+    barrier()
+    sync_all()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    stream.sync()
+    sync_all()
+    barrier()
+    mine = time.perf_counter() - t0
+    elapsed = max_over_ranks(mine)
+    g_ms = float(np.mean([e0.elapsed_ms(e1) for e0, e1 in evs]))
+    res = meta.download(12 * n, 48 * n)
+    olen, stat = res[:8 * n].view(np.uint64), res[8 * n:].view(np.int32)
+    ok = bool((stat == 0).all() and np.array_equal(olen, sizes))
+    if ok and not args.no_verify:
+        t = batch.raw_bytes
+        ok = bool(np.array_equal(batch.src.download(t), batch.out.download(t)))
+    if not ok:
+        raise SystemExit("bench: read path output is not bit-exact -- refusing to report a number")
+    raw = float(batch.raw_bytes)
+    frames = float(flen.sum())
+    alg = raw + frames
+    achieved = alg / (g_ms * 1e-3) / 1e9
+    total_raw = max_over_ranks(raw, op="sum") * args.steps
+    per_gpu = gather_ranks(raw * args.steps / mine / GIB)
+    line = {
+        "metric": "KingDB read path GiB/s (UncompressByteArray over stored values, device-resident)",
+        "value": round(total_raw / elapsed / GIB, 3), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: G1-long (db_bench CompressibleString 0.5, LevelDB Random(301)), stored as CompressorLZ4 "
+                "frames by the GPU write path's compressor",
+        "config": {"workload": f"configs[1] as a read: {n} x {size} B stored values per GPU -> values "
+                               f"(frame walk + frame decode + status pass, verify off)",
+                   "values_per_gpu": n, "value_bytes": size, "raw_bytes_per_gpu": int(raw),
+                   "parallelism": f"dp{world} (independent shards, no collective)", "ratio": round(frames / raw, 4)},
+        "roofline": {"bound": "hbm", "kernel": "kdb_get_values_batch (walk, scan, decode and finish launches)",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "alg_bytes_per_launch": int(alg), "avg_launch_ms": round(g_ms, 4)},
+        "per_gpu_gibs": [round(x, 3) for x in per_gpu],
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ns = min(n, 65536)
+        fo = batch.frame_off[:ns].astype(np.uint64)
+        span = int(fo[-1] + flen[ns - 1])
+        stored = batch.frames.download(span)
+        line["cpu_baseline"] = ref_read_path(stored, fo, flen[:ns], size, args.cpu_seconds)
+    for x in (meta, scratch):
+        x.free()
+    batch.free()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
 def bench_put(args, world: int, rank: int, local: int, barrier, sync_all) -> None:
     """configs[4]: the write path, host memory to HSTable bytes, PCIe included."""
     from kingdb_amd.lz4 import DeviceBuffer
@@ -322,8 +455,8 @@ def main() -> None:
         if world > 1:
             dist.barrier()
 
-    if args.workload == "put":
-        bench_put(args, world, rank, local, barrier, sync_all)
+    if args.workload in ("put", "get"):
+        (bench_put if args.workload == "put" else bench_get)(args, world, rank, local, barrier, sync_all)
         if world > 1:
             dist.destroy_process_group()
         return

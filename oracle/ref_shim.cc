@@ -197,3 +197,42 @@ extern "C" int ref_uncompress_value(const char* stored, uint64_t stored_len, uin
   if (s.IsOK()) return 0;
   return s.ToString().find("Invalid checksum") != std::string::npos ? 1 : 2;
 }
+
+// ---- CPU baseline for the read path (bench.py --workload get, kind "reference") ----
+// Database::GetRaw's decode step over n stored values: CompressorLZ4::
+// UncompressByteArray (verify off, ReadOptions' default) with `threads`
+// std::threads on blocked ranges, each with its own CompressorLZ4.  The
+// ByteArrays are built before the clock starts; one warm-up pass, then
+// `passes` timed passes.  Returns 0, or -1 if any value fails or differs in
+// size from `size`.
+extern "C" int ref_bench_get(const char* stored, const uint64_t* off, const uint64_t* len, int n, uint64_t size,
+                             int threads, int passes, double* seconds) {
+  std::vector<kdb::ByteArray> vals(n);
+  for (int i = 0; i < n; i++) {
+    std::vector<char> buf(len[i] + 64, 0);
+    memcpy(buf.data(), stored + off[i], len[i]);
+    vals[i] = kdb::NewDeepCopyByteArray(buf.data(), len[i] + 64);
+    kdb::NetworkTask::Set(vals[i], size, len[i], 0, 0);
+  }
+  int bad = 0;
+  auto run = [&]() {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+      th.emplace_back([&, t]() {
+        kdb::CompressorLZ4 c;
+        const int lo = (int)((int64_t)n * t / threads), hi = (int)((int64_t)n * (t + 1) / threads);
+        for (int i = lo; i < hi; i++) {
+          kdb::ByteArray o;
+          kdb::Status s = c.UncompressByteArray(vals[i], false, &o);
+          if (!s.IsOK() || o.size() != size) bad = 1;
+        }
+      });
+    }
+    for (auto& x : th) x.join();
+  };
+  run();
+  auto a = std::chrono::steady_clock::now();
+  for (int p = 0; p < passes; p++) run();
+  *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+  return bad ? -1 : 0;
+}
