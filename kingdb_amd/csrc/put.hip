@@ -28,9 +28,12 @@
 //   frame compress      the LZ4 kernels over every part (launch_compress)
 //   put_policy_kernel   thread per value: the frame policy and the entry layout
 //   scan                dense entry offsets
-//   put_entry_kernel    wave per value: key + stored chunks copied into place,
-//                       CRC32C (64-lane chunked, GF(2) tree combine), key hash,
+//   put_entry_small_kernel  thread per value, for single-part entries of at most
+//                       512 bytes of key + chunk_final: copy, CRC32C, key hash,
 //                       EntryHeader bytes
+//   put_entry_kernel    wave per value, the rest: key + stored chunks copied into
+//                       place, CRC32C (64-lane chunked, GF(2) tree combine), key
+//                       hash, EntryHeader bytes
 // The host (hstable.cc) then cuts the dense entry stream into HSTable files
 // and writes their headers and offset arrays.
 #include <hip/hip_runtime.h>
@@ -365,6 +368,84 @@ struct PutMsg {
 
 constexpr int kEntryBlock = 256;
 
+// Entries small enough for one thread: a single part (or none) and at most
+// kSmallEntry bytes of key + chunk_final -- db_bench's 16 B keys / 100 B values.
+// A wave spends on the 64-lane CRC tree and the lane-0 header what a thread
+// spends on the whole entry, so these run thread per value; the rest wave per
+// value.
+constexpr uint32_t kSmallEntry = 512;
+__device__ __forceinline__ bool small_entry(const ValueLayout& L, uint32_t np, uint32_t klen) {
+  return L.status == 0 && np <= 1u && (uint64_t)klen + L.crc_bytes <= kSmallEntry;
+}
+
+// Thread per value (small_entry values only): key and chunk_final copied into
+// place with CRC32C(key || chunk_final) (database.cc:251-257) folded into the
+// copy, the key hash, and the EntryHeader bytes with their CRC-8 emitted in
+// order (format.h:224-255, crc32c.cc:439-475).
+__global__ __launch_bounds__(256) void put_entry_small_kernel(
+    const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, const uint32_t* __restrict__ key_len,
+    const uint64_t* __restrict__ value_len, const uint32_t* __restrict__ part_first, PartSrc src,
+    const uint64_t* __restrict__ occ, const uint32_t* __restrict__ plen, const ValueLayout* __restrict__ lay,
+    uint32_t n, uint32_t hash_type, uint8_t* __restrict__ entries, const uint64_t* __restrict__ entry_off,
+    uint64_t* __restrict__ hashed, uint32_t* __restrict__ crc_out, uint32_t* __restrict__ kind_out,
+    int32_t* __restrict__ status_out) {
+  __shared__ uint32_t s_t[256];
+  __shared__ uint8_t s_c8[256];
+  crc::stage_table(s_t);
+  for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) s_c8[i] = kCrc8.t[i];
+  __syncthreads();
+  for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
+    const ValueLayout L = lay[v];
+    const uint32_t p0 = part_first[v], np = part_first[v + 1] - p0;
+    const uint32_t klen = key_len[v];
+    if (!small_entry(L, np, klen)) continue;
+    status_out[v] = 0;
+    kind_out[v] = L.kind;
+    const uint64_t V = value_len[v];
+    const uint8_t* key = keys + key_off[v];
+    const uint32_t hl = header_len(L.flags, klen, V, L.pad_hdr);
+    uint8_t* dst = entries + entry_off[v];
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < klen; i++) {
+      const uint8_t b = key[i];
+      dst[hl + i] = b;
+      c = crc::step(c, b, s_t);
+    }
+    if (np == 1u) {
+      uint8_t* vd = dst + hl + klen + occ[p0];
+      const uint32_t len = plen[p0];
+      for (uint32_t j = 0; j < len; j++) {
+        const uint8_t b = src.byte(p0, j);
+        vd[j] = b;
+        c = crc::step(c, b, s_t);
+      }
+    }
+    const uint32_t crc = c ^ 0xFFFFFFFFu;
+    const uint64_t h = hash_type == 1 ? xxh64(key, klen) : murmur3_64(key, klen);
+    hashed[v] = h;
+    crc_out[v] = crc;
+    // header bytes 1 .. hl-1 in order, each into the CRC-8, then byte 0
+    uint32_t pos = 1, c8 = 0xffu;
+    auto emit = [&](uint32_t b) {
+      dst[pos++] = (uint8_t)b;
+      c8 = s_c8[(c8 ^ b) & 0xffu];
+    };
+    auto emit_varint = [&](uint64_t x) {
+      while (x >= 128u) { emit((uint32_t)(x & 127u) | 128u); x >>= 7; }
+      emit((uint32_t)x);
+    };
+    const uint32_t cc = L.hdr_crc_final ? crc : 0u;
+    for (int i = 0; i < 4; i++) emit((cc >> (8 * i)) & 0xffu);
+    emit_varint(L.flags);
+    emit_varint(klen);
+    emit_varint(V);
+    for (int i = 0; i < 8; i++) emit((uint32_t)(L.svc_hdr >> (8 * i)) & 0xffu);
+    emit_varint(L.pad_hdr);
+    for (int i = 0; i < 8; i++) emit((uint32_t)(h >> (8 * i)) & 0xffu);
+    dst[0] = (uint8_t)(c8 ^ 0xffu);
+  }
+}
+
 // Wave per value: entry bytes at entries + entry_off[v].
 __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
     const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, const uint32_t* __restrict__ key_len,
@@ -385,9 +466,10 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
   const uint32_t nw = gridDim.x * (kEntryBlock / 64);
   for (uint32_t v = blockIdx.x * (kEntryBlock / 64) + wib; v < n; v += nw) {
     const ValueLayout L = lay[v];
+    const uint32_t klen = uni(key_len[v]);
+    if (small_entry(L, uni(part_first[v + 1]) - uni(part_first[v]), klen)) continue;   // put_entry_small_kernel's
     if (lane == 0) { status_out[v] = L.status; kind_out[v] = L.kind; }
     if (L.status != 0) continue;
-    const uint32_t klen = uni(key_len[v]);
     const uint64_t V = value_len[v];
     const uint8_t* key = keys + key_off[v];
     const uint32_t hl = header_len(L.flags, klen, V, L.pad_hdr);
@@ -497,6 +579,9 @@ hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_
   }
   const uint32_t eg = (n + 3) / 4 < 16384u ? (n + 3) / 4 : 16384u;
   PartSrc ps{values, frames, part_src, frame_off, mode};
+  const uint32_t sg = (n + 255) / 256 < 4096u ? (n + 255) / 256 : 4096u;
+  hipLaunchKernelGGL(put_entry_small_kernel, dim3(sg), dim3(256), 0, st, keys, key_off, key_len, value_len,
+                     part_first, ps, occ, plen, lay, n, hash_type, entries, entry_off, hashed, crc, kind, status);
   hipLaunchKernelGGL(put_entry_kernel, dim3(eg), dim3(kEntryBlock), 0, st, keys, key_off, key_len, value_len,
                      part_first, ps, occ, plen, lay, n, hash_type, entries, entry_off, entry_len, hashed, crc, kind,
                      status);
