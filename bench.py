@@ -59,6 +59,7 @@ def parse():
                    help="also time pinned host -> device -> host (H2D + kernels + D2H, overlapped)")
     p.add_argument("--hi-chunk", type=int, default=1 << 16, help="values per pipeline chunk")
     p.add_argument("--hi-streams", type=int, default=4)
+    p.add_argument("--put-chunk", type=int, default=1 << 17, help="put workload: puts per pipeline chunk")
     p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="HBM traffic summary written by tools/pmc_traffic.py")
     return p.parse_args()
@@ -356,7 +357,7 @@ def bench_put(args, world: int, rank: int, local: int, barrier, sync_all) -> Non
     from kingdb_amd.putpipe import PutPipeline
     from kingdb_amd.shard import gather_ranks, max_over_ranks
     n, ks, vs = args.values, 16, 100
-    pp = PutPipeline(n, ks, vs, chunk=args.hi_chunk, nstreams=args.hi_streams, direct=not args.put_host_copy)
+    pp = PutPipeline(n, ks, vs, chunk=args.put_chunk, nstreams=args.hi_streams, direct=not args.put_host_copy)
     base = rank * n                                   # this rank's slice of one global put sequence
     keys = np.frombuffer(b"".join(b"%016d" % (base + i) for i in range(n)), np.uint8).reshape(n, ks)
     pp.h_keys.np[:] = keys.reshape(-1)

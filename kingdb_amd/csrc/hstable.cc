@@ -21,8 +21,13 @@
 #include <cstdint>
 #include <cstdio>
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <vector>
@@ -81,6 +86,37 @@ uint32_t crc32c(const uint8_t* p, size_t n) {
   return l ^ 0xFFFFFFFFu;
 }
 
+// crc32c of A||B from crc32c(A), crc32c(B) and |B| (zlib's crc32_combine
+// over the Castagnoli polynomial): pieces of the offset array are checksummed
+// in parallel.
+uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
+  uint32_t sum = 0;
+  for (int i = 0; vec; vec >>= 1, i++)
+    if (vec & 1u) sum ^= mat[i];
+  return sum;
+}
+void gf2_square(uint32_t* sq, const uint32_t* mat) {
+  for (int k = 0; k < 32; k++) sq[k] = gf2_times(mat, mat[k]);
+}
+uint32_t crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  if (len2 == 0) return crc1;
+  uint32_t even[32], odd[32];
+  odd[0] = 0x82F63B78u;                     // the operator for one zero bit
+  for (int k = 1; k < 32; k++) odd[k] = 1u << (k - 1);
+  gf2_square(even, odd);                    // two zero bits
+  gf2_square(odd, even);                    // four
+  do {
+    gf2_square(even, odd);
+    if (len2 & 1u) crc1 = gf2_times(even, crc1);
+    len2 >>= 1;
+    if (!len2) break;
+    gf2_square(odd, even);
+    if (len2 & 1u) crc1 = gf2_times(odd, crc1);
+    len2 >>= 1;
+  } while (len2);
+  return crc1 ^ crc2;
+}
+
 void put32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; i++) p[i] = (uint8_t)(v >> (8 * i)); }
 void put64(uint8_t* p, uint64_t v) { for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i)); }
 uint8_t* varint(uint8_t* p, uint64_t v) {
@@ -108,8 +144,10 @@ inline uint8_t* varint_pdep(uint8_t* p, uint64_t v) {
   p[9] = 1;
   return p + len;
 }
+const bool kBmi2Host = kBmi2;
 #else
 inline uint8_t* varint_pdep(uint8_t* p, uint64_t v) { return varint(p, v); }
+const bool kBmi2Host = false;
 #endif
 
 // DatabaseOptionEncoder::EncodeTo (format.h:324-340): version 0.9.0.0, data
@@ -202,6 +240,67 @@ struct Buf {
   const uint8_t* data() const { return p; }
 };
 
+// A few persistent worker threads for the offset-array rows of large batches
+// (thread creation per batch would cost more than the work).  run(k, f) calls
+// f(0..k-1) on the workers and the caller and returns when all are done.
+class WorkPool {
+ public:
+  explicit WorkPool(unsigned workers) {
+    for (unsigned i = 0; i < workers; i++) th_.emplace_back([this] { loop(); });
+  }
+  ~WorkPool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return (unsigned)th_.size(); }
+  void run(unsigned tasks, const std::function<void(unsigned)>& f) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      fn_ = &f;
+      tasks_ = tasks;
+      next_.store(0);
+      busy_ = (unsigned)th_.size();
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [this] { return busy_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (unsigned t; (t = next_.fetch_add(1)) < tasks_;) (*fn_)(t);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> l(mu_);
+      if (--busy_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(unsigned)>* fn_ = nullptr;
+  unsigned tasks_ = 0, busy_ = 0;
+  std::atomic<unsigned> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct kdb_hstable_writer {
@@ -218,6 +317,18 @@ struct kdb_hstable_writer {
   bool padding_flag = false, incomplete = false;
   std::vector<std::pair<uint32_t, Buf>> files;   // closed files
   std::vector<Buf> spare;                   // buffers of files dropped by reset(), reused
+  std::unique_ptr<WorkPool> pool;           // row encoders for large batches (created on first use)
+  std::vector<Buf> task_rows;               // their per-task row buffers
+
+  WorkPool* workers() {
+    if (!pool) {
+      const char* e = getenv("KDB_HSTABLE_THREADS");
+      unsigned hw = std::thread::hardware_concurrency();
+      unsigned t = e && *e ? (unsigned)atoi(e) : std::min(8u, std::max(1u, hw / 2));
+      pool.reset(new WorkPool(t > 1 ? t - 1 : 0));
+    }
+    return pool.get();
+  }
 
   // every entry byte landed (DMA into the file buffers complete)
   bool settle() const {
@@ -261,20 +372,40 @@ struct kdb_hstable_writer {
     if (!open) return;
     if (!incomplete) {
       // the OffsetArrayRow::EncodeTo rows (varint64 hash, varint32 offset,
-      // encoded as the entries were appended), then the footer
+      // encoded as the entries were appended), then the footer; large arrays
+      // are copied and checksummed in pieces by the worker pool
       const size_t start = cur.size();
       if (start + rows.n + 36 > cur.cap) settle();
       cur.reserve(start + rows.n + 36);
       uint8_t* q = cur.data() + start;
-      memcpy(q, rows.data(), rows.n);
+      uint32_t crc_rows = 0;
+      constexpr size_t kPiece = 1u << 20;
+      if (rows.n >= 2 * kPiece) {
+        const unsigned pieces = (unsigned)((rows.n + kPiece - 1) / kPiece);
+        std::vector<uint32_t> pc(pieces);
+        const uint8_t* r = rows.data();
+        const size_t total = rows.n;
+        const std::function<void(unsigned)> f = [&](unsigned k) {
+          const size_t a = (size_t)k * kPiece, b = std::min(total, a + kPiece);
+          memcpy(q + a, r + a, b - a);
+          pc[k] = crc32c(q + a, b - a);
+        };
+        workers()->run(pieces, f);
+        crc_rows = pc[0];
+        for (unsigned k = 1; k < pieces; k++)
+          crc_rows = crc32c_combine(crc_rows, pc[k], std::min(total, (size_t)(k + 1) * kPiece) - (size_t)k * kPiece);
+      } else {
+        memcpy(q, rows.data(), rows.n);
+        crc_rows = crc32c(q, rows.n);
+      }
       q += rows.n;
       put32(q, 1);
       put32(q + 4, padding_flag ? 1u : 0u);
       put64(q + 8, start);
       put64(q + 16, nrows);
       put64(q + 24, kMagic);
+      put32(q + 32, crc32c_combine(crc_rows, crc32c(q, 32), 32));
       q += 32;
-      put32(q, crc32c(cur.data() + start, (size_t)(q - (cur.data() + start))));
       cur.n = (size_t)(q + 4 - cur.data());
     }
     files.emplace_back(fileid, std::move(cur));
@@ -305,8 +436,109 @@ int kdb_hstable_writer_create(uint64_t hstable_size, uint32_t hash_type, kdb_hst
 
 namespace {
 
-// WriteOrdersAndFlushFile over one batch; `land(dst, src_off, len)` puts the
-// dense stream's bytes [src_off, src_off+len) at dst (host memcpy, or DMA).
+// Batches of plain entries (every status 0, kind 0, entries back to back in
+// the dense stream -- a write-buffer flush of small puts): the same files as
+// append_loop, with the work split differently.  File cuts come from the dense
+// offsets by binary search; the offset-array rows are encoded by the worker
+// pool, one task per slice of a file's entries, and checked for the
+// conditions on the way; then the rows, the entry bytes (one run per file)
+// and the file opens/closes are committed in order.  Returns 1 (nothing done)
+// when the conditions fail, for append_loop to take the batch.
+constexpr uint32_t kFastMin = 4096;
+template <class Land>
+int append_fast(kdb_hstable_writer* w, const uint64_t* off, const uint32_t* len, const uint64_t* hashed,
+                const uint32_t* kind, const int32_t* status, uint32_t n, Land& land) {
+  const uint64_t sb = w->size_block;
+  const uint64_t span = off[n - 1] + len[n - 1] - off[0];
+  if (off[n - 1] < off[0] || sb + span + kHeaderSize > 0xFFFFFFFFull) return 1;
+  struct Seg {
+    uint32_t a, b;
+    uint64_t fs;                 // offset_end_ before entry a
+    bool close_first, open_first;
+  };
+  std::vector<Seg> segs;
+  bool open = w->open;
+  uint64_t fs = open ? w->cur.size() : 0;
+  for (uint32_t i = 0; i < n;) {
+    Seg g{i, 0, 0, false, false};
+    if (open && fs > sb) {                  // FlushCurrentFile(true, 0) before entry i
+      g.close_first = true;
+      open = false;
+    }
+    if (!open) {
+      g.open_first = true;
+      open = true;
+      fs = kHeaderSize;
+    }
+    // entries stay while offset_end_ before them is <= size_block
+    const uint64_t lim = off[i] + (sb - fs);
+    const uint32_t j = (uint32_t)(std::upper_bound(off + i + 1, off + n, lim) - off);
+    g.b = j;
+    g.fs = fs;
+    segs.push_back(g);
+    fs += off[j - 1] + len[j - 1] - off[i];
+    i = j;
+  }
+  // tasks: slices of each segment
+  WorkPool* pool = w->workers();
+  const uint32_t per = std::max<uint32_t>(2048u, n / (4u * (pool->size() + 1u)) + 1u);
+  struct Task { uint32_t a, b, seg; };
+  std::vector<Task> tasks;
+  for (uint32_t k = 0; k < segs.size(); k++)
+    for (uint32_t a = segs[k].a; a < segs[k].b; a += per) tasks.push_back({a, std::min(segs[k].b, a + per), k});
+  if (w->task_rows.size() < tasks.size()) w->task_rows.resize(tasks.size());
+  std::atomic<bool> bad{false};
+  const bool pdep = kBmi2Host;
+  const std::function<void(unsigned)> enc = [&](unsigned t) {
+    const Task tk = tasks[t];
+    const uint64_t base = segs[tk.seg].fs - off[segs[tk.seg].a];
+    Buf& r = w->task_rows[t];
+    r.reserve((size_t)(tk.b - tk.a) * 15u + 32u);
+    uint8_t* __restrict__ p = r.data();
+    const uint64_t* __restrict__ o = off;
+    const uint32_t* __restrict__ l = len;
+    const uint64_t* __restrict__ h = hashed;
+    uint32_t bad_any = 0;
+    for (uint32_t i = tk.a; i < tk.b; i++) bad_any |= (uint32_t)status[i] | kind[i];
+    const uint32_t last = tk.b == n ? tk.b - 1 : tk.b;      // entries i with a successor to check
+    for (uint32_t i = tk.a; i < last; i++) bad_any |= (uint32_t)(o[i + 1] != o[i] + l[i]);
+    if (pdep) {
+      for (uint32_t i = tk.a; i < tk.b; i++) {
+        p = varint_pdep(p, h[i]);
+        p = varint_pdep(p, base + o[i]);
+      }
+    } else {
+      for (uint32_t i = tk.a; i < tk.b; i++) {
+        p = varint(p, h[i]);
+        p = varint(p, base + o[i]);
+      }
+    }
+    r.n = (size_t)(p - r.data());
+    if (bad_any) bad = true;
+  };
+  pool->run((unsigned)tasks.size(), enc);
+  if (bad) return 1;
+  uint32_t t = 0;
+  for (uint32_t k = 0; k < segs.size(); k++) {
+    const Seg& g = segs[k];
+    if (g.close_first) w->close_file();
+    if (g.open_first) w->open_file();
+    for (; t < tasks.size() && tasks[t].seg == k; t++) {
+      const Buf& r = w->task_rows[t];
+      w->rows.reserve(std::max(w->rows.n + r.n + 32, w->rows.cap));
+      memcpy(w->rows.data() + w->rows.n, r.data(), r.n);
+      w->rows.n += r.n;
+      w->nrows += tasks[t].b - tasks[t].a;
+    }
+    const int rc = land(w, off[g.a], off[g.b - 1] + len[g.b - 1] - off[g.a]);
+    if (rc != KDB_PUT_OK) return rc;
+  }
+  if (w->open && w->cur.size() >= sb) w->close_file();    // end of batch: FlushCurrentFile(0, 0)
+  return KDB_PUT_OK;
+}
+
+// WriteOrdersAndFlushFile entry by entry (any batch: failed puts, multipart
+// kinds, non-dense streams).
 template <bool kPdep, class Land>
 int append_loop(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t* entry_len, const uint64_t* hashed,
                 const uint32_t* kind, const int32_t* status, uint32_t n, Land land) {
@@ -407,6 +639,14 @@ int append_loop(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t
 template <class Land>
 int append_batch(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t* entry_len, const uint64_t* hashed,
                  const uint32_t* kind, const int32_t* status, uint32_t n, Land land) {
+  static const bool serial = [] {
+    const char* e = getenv("KDB_HSTABLE_SERIAL");     // diagnostic: one thread, entry by entry
+    return e && *e && *e != '0';
+  }();
+  if (!serial && n >= kFastMin) {
+    const int rc = append_fast(w, entry_off, entry_len, hashed, kind, status, n, land);
+    if (rc != 1) return rc;
+  }
 #if defined(__x86_64__)
   if (kBmi2) return append_loop<true>(w, entry_off, entry_len, hashed, kind, status, n, land);
 #endif

@@ -83,6 +83,54 @@ def test_host_hstable_writer_matches_reference(orc, name):
         assert got[f] == files[f], f
 
 
+@pytest.mark.parametrize("hs,batch", [(96 << 10, 6000), (32 << 20, 20000), (1 << 20, 4096)])
+def test_host_hstable_writer_parallel_batches(orc, hs, batch):
+    """Batches of >= 4096 plain entries take the writer's parallel path (file
+    cuts by binary search over the dense offsets, rows encoded by the worker
+    pool); the files must equal the oracle's for the same write-buffer flushes,
+    with files cut inside and across batches.  A batch with a failed put falls
+    back to the entry-by-entry path."""
+    import oracle
+    from oracle import hstable
+    from kingdb_amd.put import HSTableWriter, PutBatchResult
+    n = 20000
+    pool = oracle.g1_pool(orc)
+    vals = oracle.g1_values(pool, 100, n)
+    puts = [(b"%016d" % i, v, None) for i, v in enumerate(vals)]
+    w = hstable.Writer(orc, hs, 1)
+    for lo in range(0, n, batch):
+        for k, v, ch in puts[lo:lo + batch]:
+            w.put(k, v, ch)
+        w._flush(0, 0)
+    files = w.close()
+    dense = w.dense()
+    assert len(dense) == n
+    hw = HSTableWriter(hs, 1)
+    for lo in range(0, n, batch):
+        d = dense[lo:lo + batch]
+        lens = np.array([len(e) for e, _, _ in d], np.uint32)
+        off = np.zeros(len(d), np.uint64)
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        st = np.zeros(len(d), np.int32)
+        ents = b"".join(e for e, _, _ in d)
+        if lo == 0 and batch == 4096:
+            # a failed put (IOError: no order, no bytes in the stream) -> the serial path
+            st = np.append(st, -1).astype(np.int32)
+            lens = np.append(lens, 0).astype(np.uint32)
+            off = np.append(off, off[-1] + lens[-2]).astype(np.uint64)
+        hashes = [h for _, h, _ in d] + ([0] * (len(st) - len(d)))
+        kinds = [k for _, _, k in d] + ([0] * (len(st) - len(d)))
+        r = PutBatchResult(entries=np.frombuffer(ents, np.uint8).copy(), entry_off=off, entry_len=lens,
+                           hashed=np.array(hashes, np.uint64), crc=np.zeros(len(st), np.uint32),
+                           kind=np.array(kinds, np.uint32), status=st)
+        hw.append(r)
+    hw.close()
+    got = hw.files()
+    assert list(got) == list(files)
+    for f in files:
+        assert got[f] == files[f], f
+
+
 def test_db_options_bytes(orc):
     from kingdb_amd.put import db_options
     from oracle import hstable
