@@ -12,10 +12,11 @@
 namespace kdb_lz4 {
 
 namespace {
-// Per-device pool of 16-byte counter slots.  A launch takes the next slot
-// round-robin and zeroes it on its own stream (stream-ordered, so a slot is
-// reused only after 4096 later launches -- far more than can be in flight).
-constexpr uint32_t kSlots = 4096;
+// Per-device pool of 512-byte counter slots (a WorkQueue's 8 counters, 64 B
+// apart).  A launch takes the next slot round-robin and zeroes it on its own
+// stream (a slot is reused only after 2048 later launches -- far more than
+// can be in flight).
+constexpr uint32_t kSlots = 2048, kSlotBytes = 512;
 struct Pool {
   uint8_t* base = nullptr;
   std::atomic<uint32_t> next{0};
@@ -34,7 +35,7 @@ hipError_t work_counter(hipStream_t st, uint32_t** ctr) {
     Pool*& slot = g_pools[dev];
     if (!slot) {
       slot = new Pool();
-      e = hipMalloc(&slot->base, (size_t)kSlots * 16u);
+      e = hipMalloc(&slot->base, (size_t)kSlots * kSlotBytes);
       if (e != hipSuccess) {
         delete slot;
         slot = nullptr;
@@ -43,8 +44,8 @@ hipError_t work_counter(hipStream_t st, uint32_t** ctr) {
     }
     p = slot;
   }
-  uint8_t* c = p->base + (size_t)(p->next.fetch_add(1) % kSlots) * 16u;
-  e = hipMemsetAsync(c, 0, 16, st);
+  uint8_t* c = p->base + (size_t)(p->next.fetch_add(1) % kSlots) * kSlotBytes;
+  e = hipMemsetAsync(c, 0, kSlotBytes, st);
   *ctr = reinterpret_cast<uint32_t*>(c);
   return e;
 }
@@ -116,6 +117,20 @@ hipError_t fork_end(hipStream_t st, hipStream_t aux) {
   Fork& f = t_fork[dev];
   if ((e = hipEventRecord(f.join, aux)) != hipSuccess) return e;
   return hipStreamWaitEvent(st, f.join, 0);
+}
+
+// Ranges per launch.  Tiny values saturate one counter (128 Ki 100-byte
+// values: ~70 claims/us), and even at 4 KiB, where the rate is far below
+// that, a contended counter's latency shows: decompress 5.79 ms with one
+// range vs 5.30 ms with eight (1 Mi x 4 KiB).  So: eight, unless overridden.
+uint32_t work_queues(uint32_t max_len) {
+  (void)max_len;
+  static const int env = [] {
+    const char* e = getenv("KDB_LZ4_QUEUES");      // diagnostic: force 1 or 8 ranges
+    return e && *e ? atoi(e) : 0;
+  }();
+  if (env > 0) return (uint32_t)env;
+  return 8u;   // kQueues (lz4_device.h)
 }
 
 // Values per counter claim: ~1/8 of a workgroup's share, at most 16, so the

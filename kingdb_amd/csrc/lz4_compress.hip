@@ -465,7 +465,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
     int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
-    uint32_t cls) {
+    uint32_t cls, uint32_t nq) {
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   // register prefetch (kSmall): the next value's realigned 16-byte chunks
   uint4 pa[kPrefetch], pb[kPrefetch];
   uint32_t p_head = 0, p_chunks = 0;
-  WorkQueue wq{work, n, batch, 0u, 0u};
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq);
   uint32_t v = wq.next();
   auto prefetch = [&](uint32_t w) {
     if (w < n) {
@@ -676,7 +676,7 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
-                     dst_cap, frame_len, ret, work, batch, census, cls);
+                     dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap));
   return hipGetLastError();
 }
 

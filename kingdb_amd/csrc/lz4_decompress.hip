@@ -214,7 +214,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t skip_big) {
+    uint32_t skip_big, uint32_t nq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   // [staged block + 16 zero bytes][output window + 64 bytes of slack for the
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
   uint8_t* s_in = smem;
   uint8_t* s_out = smem + (((size_t)in_cap + 32u + 15u) & ~(size_t)15u);
 
-  WorkQueue wq{work, n, batch, 0u, 0u};
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq);
 #pragma unroll 1
   for (uint32_t v = wq.next(); v < n; v = wq.next()) {
     const uint8_t* g = src + src_off[v];
@@ -680,7 +680,7 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
-                     out_cap, target, out_len, ret, work, batch, skip_big);
+                     out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out));
   return hipGetLastError();
 }
 

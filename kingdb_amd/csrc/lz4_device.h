@@ -53,23 +53,46 @@ __device__ __forceinline__ uint32_t first_zero(uint64_t m) {
 }
 
 // Dynamic work distribution of the persistent kernels.  Lane 0 claims `batch`
-// consecutive value indices with one device-scope atomic; a single counter
-// saturates near 88 claims/us (microarch "dequeue"), so claims are batched to
-// stay far below that.  next() hands out values one ahead of their use.
+// consecutive value indices with one device-scope atomic.  A single counter
+// saturates near 88 claims/us (microarch "dequeue") -- a launch of 128 Ki
+// 100-byte values was bound by exactly that -- so the index space is split
+// into kQueues ranges with a counter each (64 bytes apart): a workgroup starts
+// on range blockIdx % kQueues and moves to the next range when its own is
+// exhausted (a plain load first, so finished ranges cost no atomics).
+// next() hands out values one ahead of their use.
+constexpr uint32_t kQueues = 8, kQueueStride = 16;   // counters: 8 x u32, 64 B apart (work_counter slots)
 struct WorkQueue {
   uint32_t* ctr;
-  uint32_t n, batch, cur, end;
-  __device__ __forceinline__ void claim() {
-    uint32_t v = 0;
-    if (lane_id() == 0) v = atomicAdd(ctr, batch);
-    cur = uni(v);
-    end = min(cur + batch, n);
+  uint32_t n, batch, cur, end, nr, q, left;
+  // nr ranges: 1, or kQueues for launches whose claim rate would saturate one
+  // counter (work_queues() on the host picks)
+  __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr) {
+    nr = nr > 1u ? kQueues : 1u;
+    return WorkQueue{c, n, batch, 0u, 0u, nr, (uint32_t)blockIdx.x % nr, nr};
   }
-  __device__ __forceinline__ uint32_t next() {   // n when the batch is exhausted
+  __device__ __forceinline__ void claim() {
+    while (left) {
+      const uint32_t lo = (uint32_t)((uint64_t)n * q / nr), hi = (uint32_t)((uint64_t)n * (q + 1u) / nr);
+      uint32_t v = 0;
+      if (lane_id() == 0) {
+        uint32_t* c = ctr + kQueueStride * q;
+        v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi - lo ? atomicAdd(c, batch) : hi - lo;
+      }
+      v = uni(v);
+      if (v < hi - lo) {
+        cur = lo + v;
+        end = min(cur + batch, hi);
+        return;
+      }
+      q = q + 1u == nr ? 0u : q + 1u;
+      left--;
+    }
+    cur = end = n;
+  }
+  __device__ __forceinline__ uint32_t next() {   // n when every range is exhausted
     if (cur >= end) {
-      if (end >= n && cur >= n) return n;
       claim();
-      if (cur >= n) return n;
+      if (cur >= end) return n;
     }
     return cur++;
   }
@@ -132,6 +155,8 @@ __device__ __forceinline__ void flush_lds_to_global(uint8_t* g, const uint8_t* l
 hipError_t work_counter(hipStream_t st, uint32_t** ctr);
 uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
 uint32_t claim_batch(uint32_t n, uint32_t grid);
+// WorkQueue ranges for a launch whose values are at most max_len bytes
+uint32_t work_queues(uint32_t max_len);
 // size-class launches on a second stream: *aux waits for st's work so far;
 // fork_end makes st wait for aux (KDB_LZ4_NOFORK=1: aux == st)
 hipError_t fork_begin(hipStream_t st, hipStream_t* aux);
