@@ -209,6 +209,17 @@ struct ValueLayout {
   int32_t status;         // 0, or -1 (IOError)
 };
 
+// Entries small enough for one thread: a single part (or none) and at most
+// kSmallEntry bytes of key + chunk_final -- db_bench's 16 B keys / 100 B values.
+// A wave spends on the 64-lane CRC tree and the lane-0 header what a thread
+// spends on the whole entry, so these run thread per value; the rest wave per
+// value
+// (the policy kernel lists the latter in `big`: count, then value indices).
+constexpr uint32_t kSmallEntry = 512;
+__device__ __forceinline__ bool small_entry(const ValueLayout& L, uint32_t np, uint32_t klen) {
+  return L.status == 0 && np <= 1u && (uint64_t)klen + L.crc_bytes <= kSmallEntry;
+}
+
 // Thread per value: raw offset of each part and its frame slot size.
 __global__ void put_prep_kernel(const uint64_t* __restrict__ value_off, const uint32_t* __restrict__ part_first,
                                 const uint32_t* __restrict__ chunk_len, uint32_t n, uint64_t* __restrict__ part_src,
@@ -231,7 +242,7 @@ __global__ void put_policy_kernel(const uint32_t* __restrict__ key_len, const ui
                                   const uint32_t* __restrict__ frame_len, const int32_t* __restrict__ fstatus,
                                   uint32_t n, uint64_t* __restrict__ occ, uint32_t* __restrict__ plen,
                                   uint32_t* __restrict__ mode, ValueLayout* __restrict__ lay,
-                                  uint32_t* __restrict__ entry_len) {
+                                  uint32_t* __restrict__ entry_len, uint32_t* __restrict__ big) {
   for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < n; v += gridDim.x * blockDim.x) {
     const uint64_t V = value_len[v];
     const uint64_t pad = padding_size(V);
@@ -284,6 +295,7 @@ __global__ void put_policy_kernel(const uint32_t* __restrict__ key_len, const ui
       L.kind = 0;
       lay[v] = L;
       entry_len[v] = 0;
+      big[1u + atomicAdd(big, 1u)] = v;          // its status is the wave kernel's to write
       continue;
     }
     // HSTableManager over the orders: order i carries size_value_compressed and
@@ -326,6 +338,7 @@ __global__ void put_policy_kernel(const uint32_t* __restrict__ key_len, const ui
       entry_len[v] = header_len(L.flags, klen, V, pad) + klen + (uint32_t)(V + pad);
     }
     lay[v] = L;
+    if (!small_entry(L, np, klen)) big[1u + atomicAdd(big, 1u)] = v;
   }
 }
 
@@ -368,15 +381,6 @@ struct PutMsg {
 
 constexpr int kEntryBlock = 256;
 
-// Entries small enough for one thread: a single part (or none) and at most
-// kSmallEntry bytes of key + chunk_final -- db_bench's 16 B keys / 100 B values.
-// A wave spends on the 64-lane CRC tree and the lane-0 header what a thread
-// spends on the whole entry, so these run thread per value; the rest wave per
-// value.
-constexpr uint32_t kSmallEntry = 512;
-__device__ __forceinline__ bool small_entry(const ValueLayout& L, uint32_t np, uint32_t klen) {
-  return L.status == 0 && np <= 1u && (uint64_t)klen + L.crc_bytes <= kSmallEntry;
-}
 
 // Thread per value (small_entry values only): key and chunk_final copied into
 // place with CRC32C(key || chunk_final) (database.cc:251-257) folded into the
@@ -406,16 +410,26 @@ __global__ __launch_bounds__(256) void put_entry_small_kernel(
     const uint32_t hl = header_len(L.flags, klen, V, L.pad_hdr);
     uint8_t* dst = entries + entry_off[v];
     uint32_t c = 0xFFFFFFFFu;
+    // (sources resolved once: byte stores through dst may alias anything, so
+    // the compiler would reload the part's mode and offsets per byte)
     for (uint32_t i = 0; i < klen; i++) {
       const uint8_t b = key[i];
       dst[hl + i] = b;
       c = crc::step(c, b, s_t);
     }
     if (np == 1u) {
-      uint8_t* vd = dst + hl + klen + occ[p0];
+      const uint32_t m = src.mode[p0] & kModeMask;
       const uint32_t len = plen[p0];
-      for (uint32_t j = 0; j < len; j++) {
-        const uint8_t b = src.byte(p0, j);
+      uint8_t* vd = dst + hl + klen + occ[p0];
+      // chunk_final byte j = cb[j - skip] for j >= skip, 0 below (the disable header)
+      const uint32_t skip = m == kModeDisabled ? 8u : 0u;
+      const uint8_t* cb = m == kModeFrame ? src.frames + src.frame_off[p0] : src.values + src.part_src[p0];
+      for (uint32_t j = 0; j < skip && j < len; j++) {
+        vd[j] = 0;
+        c = crc::step(c, 0u, s_t);
+      }
+      for (uint32_t j = skip; j < len; j++) {
+        const uint8_t b = cb[j - skip];
         vd[j] = b;
         c = crc::step(c, b, s_t);
       }
@@ -453,7 +467,9 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
     const uint64_t* __restrict__ occ, const uint32_t* __restrict__ plen, const ValueLayout* __restrict__ lay,
     uint32_t n, uint32_t hash_type, uint8_t* __restrict__ entries, const uint64_t* __restrict__ entry_off,
     const uint32_t* __restrict__ entry_len, uint64_t* __restrict__ hashed, uint32_t* __restrict__ crc_out,
-    uint32_t* __restrict__ kind_out, int32_t* __restrict__ status_out) {
+    uint32_t* __restrict__ kind_out, int32_t* __restrict__ status_out, const uint32_t* __restrict__ big) {
+  const uint32_t nbig = big[0];
+  if (blockIdx.x * (kEntryBlock / 64) >= nbig) return;
   __shared__ uint32_t s_t[256];
   __shared__ uint8_t s_c8[256];
   __shared__ uint8_t s_hdr[kEntryBlock / 64][64];
@@ -464,10 +480,10 @@ __global__ __launch_bounds__(kEntryBlock) void put_entry_kernel(
   const uint32_t wib = threadIdx.x / 64u;
   uint8_t* hdr = s_hdr[wib];
   const uint32_t nw = gridDim.x * (kEntryBlock / 64);
-  for (uint32_t v = blockIdx.x * (kEntryBlock / 64) + wib; v < n; v += nw) {
+  for (uint32_t i = blockIdx.x * (kEntryBlock / 64) + wib; i < nbig; i += nw) {
+    const uint32_t v = uni(big[1u + i]);
     const ValueLayout L = lay[v];
     const uint32_t klen = uni(key_len[v]);
-    if (small_entry(L, uni(part_first[v + 1]) - uni(part_first[v]), klen)) continue;   // put_entry_small_kernel's
     if (lane == 0) { status_out[v] = L.status; kind_out[v] = L.kind; }
     if (L.status != 0) continue;
     const uint64_t V = value_len[v];
@@ -526,9 +542,9 @@ __global__ void zero_u64_kernel(uint64_t* p) { *p = 0; }
 uint64_t put_scratch_bytes(uint32_t n, uint32_t nparts, uint64_t raw_bytes) {
   const uint64_t frames = raw_bytes + raw_bytes / 255u + (uint64_t)nparts * 40u + 64u;
   const uint64_t parts = (uint64_t)nparts * (8 + 4 + 8 + 4 + 4 + 8 + 4 + 4);
-  const uint64_t vals = (uint64_t)n * (sizeof(ValueLayout) + 8) + 64u;
-  // every array of launch_put_entries starts on a 256-byte boundary: 12 arrays
-  return frames + parts + vals + 12u * 256u;
+  const uint64_t vals = (uint64_t)n * (sizeof(ValueLayout) + 8 + 4) + 64u;
+  // every array of launch_put_entries starts on a 256-byte boundary: 13 arrays
+  return frames + parts + vals + 13u * 256u;
 }
 
 hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_t* key_off, const uint32_t* key_len,
@@ -556,6 +572,7 @@ hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_
   uint32_t* mode = reinterpret_cast<uint32_t*>(take((uint64_t)nparts * 4u));
   ValueLayout* lay = reinterpret_cast<ValueLayout*>(take((uint64_t)n * sizeof(ValueLayout)));
   uint64_t* ftotal = reinterpret_cast<uint64_t*>(take(8));
+  uint32_t* big = reinterpret_cast<uint32_t*>(take(4u + (uint64_t)n * 4u));   // count, then value indices
   (void)part_slot;
   if (n == 0) {
     hipLaunchKernelGGL(zero_u64_kernel, dim3(1), dim3(1), 0, st, total);
@@ -571,8 +588,12 @@ hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_
                                    nullptr, frame_len, fstatus);
     if (e != hipSuccess) return e;
   }
+  {
+    const hipError_t e = hipMemsetAsync(big, 0, 4, st);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(put_policy_kernel, dim3(tg), dim3(tb), 0, st, key_len, value_len, part_first, chunk_len,
-                     frame_len, fstatus, n, occ, plen, mode, lay, entry_len);
+                     frame_len, fstatus, n, occ, plen, mode, lay, entry_len, big);
   {
     const hipError_t e = launch_exclusive_scan(st, entry_len, n, entry_off, total);
     if (e != hipSuccess) return e;
@@ -584,7 +605,7 @@ hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_
                      part_first, ps, occ, plen, lay, n, hash_type, entries, entry_off, hashed, crc, kind, status);
   hipLaunchKernelGGL(put_entry_kernel, dim3(eg), dim3(kEntryBlock), 0, st, keys, key_off, key_len, value_len,
                      part_first, ps, occ, plen, lay, n, hash_type, entries, entry_off, entry_len, hashed, crc, kind,
-                     status);
+                     status, big);
   return hipGetLastError();
 }
 
