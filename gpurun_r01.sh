@@ -20,10 +20,14 @@ cat gpurun_out/mixed.json
 step put
 timeout -k 10 400 python bench.py --workload put > gpurun_out/put.json 2> gpurun_out/put.err || { echo "put rc=$?"; tail -20 gpurun_out/put.err; exit 1; }
 cat gpurun_out/put.json
+step get
+timeout -k 10 300 python bench.py --workload get > gpurun_out/get.json 2> gpurun_out/get.err || { echo "get rc=$?"; tail -20 gpurun_out/get.err; exit 1; }
+cat gpurun_out/get.json
 step rocprof
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --steps 5 --warmup 1 > gpurun_out/prof_bench.json 2> gpurun_out/prof.err || { echo "rocprof rc=$?"; tail -20 gpurun_out/prof.err; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_mixed" -o mixed -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload mixed --steps 3 --warmup 1 > gpurun_out/prof_mixed.json 2> gpurun_out/prof_mixed.err || { echo "rocprof mixed rc=$?"; tail -20 gpurun_out/prof_mixed.err; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_put" -o put -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload put --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/prof_put.json 2> gpurun_out/prof_put.err || { echo "rocprof put rc=$?"; tail -20 gpurun_out/prof_put.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_get" -o get -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload get --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/prof_get.json 2> gpurun_out/prof_get.err || { echo "rocprof get rc=$?"; tail -20 gpurun_out/prof_get.err; exit 1; }
 step pmc
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c" -o pmc -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --no-verify --steps 1 --warmup 0 > gpurun_out/pmc_$c.log 2>&1 || { echo "pmc $c rc=$?"; tail -20 gpurun_out/pmc_$c.log; exit 1; }

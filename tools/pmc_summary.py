@@ -11,7 +11,7 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
         k = row.get("Kernel_Name", "?")
-        short = k.split("(")[0].replace("void ", "")
+        short = k.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         vals[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, cs in vals.items():
     if "gen_g1" in k:
