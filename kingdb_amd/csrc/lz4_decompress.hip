@@ -54,6 +54,11 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
   in_off = uni(in_off);
   const int iend = unii(csize), oend = unii(osize);
   const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
+  // fast-path bounds: a sequence starting at ip <= far_ip (<= 62 header and
+  // literal bytes, then 3 more) is not the last by input; at op <= far_op its
+  // literals stay under oexit and its match (<= 273 bytes) under oend - 5
+  const int far_ip = iend - (int)(2 + 1 + kLastLiterals) - 62;
+  const int far_op = min(oexit - 60, oend - (int)kLastLiterals - 60 - 273);
   const uint8_t* in = lds_in + in_off;
   Window wd{reinterpret_cast<const uint32_t*>(lds_in), 0u, 0u};
   wd.load(in_off);
@@ -77,25 +82,26 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // token (v_readlane), instead of scalar window reads.  Anything else --
       // and every error, so its exact code -- goes through the general path
       // below from the same token.
-      // (conditions as sign bits of plain integers: one scalar compare each,
-      // instead of a chain of 64-bit lane-mask selects)
+      // Every scalar instruction counts here (the decoder issues about one per
+      // CU cycle), so the bounds are folded into one "far from both ends"
+      // test per sequence -- ip <= far_ip, op <= far_op make the not-last
+      // and output checks of any fast sequence true (lit <= 60, mlen <= 273)
+      // -- and the rest are sign bits of plain integer expressions, one
+      // compare per group, not chains of 64-bit lane-mask selects.
       const int tk = (int)(q & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((q >> 8) & 0xffu);
       const int lx = (ln + 1) >> 4;                               // a literal-length byte follows
-      const int lit = ln + (lx ? b1 : 0);
-      const int ls = ip + 1 + lx;
-      const int opl = op + lit;
-      // ok: (ln < 15 || b1 < 255); bad: lit > 60 || opl > oexit || not-last fails
-      const int ok1 = (ln - (int)kRunMask) | (b1 - 255);
-      const int bad1 = (60 - lit) | (oexit - opl) | (iend - (int)(2 + 1 + kLastLiterals) - ls - lit);
-      if ((ok1 & ~bad1) < 0) {
+      const int xl = b1 & -lx;                                    // its value, or 0
+      const int lit = ln + xl;                                    // <= 60 iff !lx || b1 <= 45
+      if (((far_ip - ip) | (far_op - op) | (45 - xl)) >= 0) {
+        const int ls = ip + 1 + lx;
+        const int opl = op + lit;
         const uint32_t v = in[ls + (int)lane];
         const int e = (int)readlane(v, (uint32_t)lit + 2u);
         const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
         const int mx = (mn + 1) >> 4;                             // a match-length byte follows
-        const int mlen = mn + (mx ? e : 0) + (int)kMinMatch;
-        const int ok2 = (mn - (int)kMlMask) | (e - 255);
-        const int bad2 = (opl - off) | (oend - (int)kLastLiterals - opl - mlen);
-        if ((ok2 & ~bad2) < 0) {
+        const int xm = e & -mx;
+        const int mlen = mn + xm + (int)kMinMatch;
+        if (((opl - off) | (254 - xm)) >= 0) {                    // ref >= 0; one match-length byte
           out[op + (int)lane] = (uint8_t)v;        // lz4.cc:947 (lanes past lit: not-yet-produced output)
           const uint32_t nt = (uint32_t)(lit + 2 + mx);             // next token's lane (<= 63)
           q = readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8);
@@ -114,8 +120,12 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
               }
             }
           } else {
+            // the first 64-byte step unconditionally (mlen >= 4), the rest only for long matches
+            const uint8_t b0 = out[ref + (int)lane];
+            out[opl + (int)lane] = b0;
+            asm volatile("" ::: "memory");
 #pragma unroll 1
-            for (int i = 0; i < mlen; i += 64) {
+            for (int i = 64; i < mlen; i += 64) {
               const uint8_t b = out[ref + i + (int)lane];
               out[opl + i + (int)lane] = b;
               asm volatile("" ::: "memory");
@@ -367,6 +377,8 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
   const uint32_t lane = lane_id();
   const int iend = unii(csize), oend = unii(osize);
   const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
+  const int far_ip = iend - (int)(2 + 1 + kLastLiterals) - 62;   // as in decode_block
+  const int far_op = min(oexit - 60, oend - (int)kLastLiterals - 60 - 273);
   RingWindow wd{reinterpret_cast<const uint32_t*>(in.lds), 0u, 0u};
   wd.invalidate();
   in.ensure(kIRing);
@@ -389,20 +401,18 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
       // sources), and the match source must lie in the output ring.
       const int tk = (int)(q & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((q >> 8) & 0xffu);
       const int lx = (ln + 1) >> 4;
-      const int lit = ln + (lx ? b1 : 0);
-      const int ls = ip + 1 + lx;
-      const int opl = op + lit;
-      const int ok1 = (ln - (int)kRunMask) | (b1 - 255);
-      const int bad1 = (60 - lit) | (oexit - opl) | (iend - (int)(2 + 1 + kLastLiterals) - ls - lit);
-      if ((ok1 & ~bad1) < 0) {
+      const int xl = b1 & -lx;
+      const int lit = ln + xl;
+      if (((far_ip - ip) | (far_op - op) | (45 - xl)) >= 0) {
+        const int ls = ip + 1 + lx;
+        const int opl = op + lit;
         const uint32_t v = in.lds[((uint32_t)ls & kIMask) + lane];
         const int e = (int)readlane(v, (uint32_t)lit + 2u);
         const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
         const int mx = (mn + 1) >> 4;
-        const int mlen = mn + (mx ? e : 0) + (int)kMinMatch;
-        const int ok2 = (mn - (int)kMlMask) | (e - 255);
-        const int bad2 = (opl - off) | (oend - (int)kLastLiterals - opl - mlen) | ((int)kORing - off);
-        if ((ok2 & ~bad2) < 0) {
+        const int xm = e & -mx;
+        const int mlen = mn + xm + (int)kMinMatch;
+        if (((opl - off) | (254 - xm) | ((int)kORing - off)) >= 0) {
           if ((int)lane < lit) {
             ring[(uint32_t)(op + (int)lane) & kOMask] = (uint8_t)v;
             o[op + (int)lane] = (uint8_t)v;
