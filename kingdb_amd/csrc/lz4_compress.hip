@@ -33,6 +33,7 @@
 //    measured from the original position, so neither waits for the other;
 //  * the byte emission of a sequence.
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "lz4_device.h"
@@ -192,14 +193,73 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
+// Same-slot grouping of a search chunk: for each lane, the valid lanes of the
+// chunk whose positions hash to its table slot (itself included).
+//
+// BallotGroup: bit-sliced match-any, one ballot per hash bit.
+template <int kHashBits>
+struct BallotGroup {
+  __device__ __forceinline__ uint64_t same(uint32_t h, bool, uint64_t vm) const {
+    uint32_t lo = ~0u, hi = ~0u;
+#pragma unroll
+    for (int bb = 0; bb < kHashBits; bb += 2) {
+      // t = 0 or ~0 (one v_bfe_i32); the empty asm keeps the ballot on t
+      // itself instead of a second shift + compare of h.  Bits go in pairs
+      // so each ballot's SGPR write is not read by the very next VALU op
+      // (no s_nop wait states).
+      uint32_t t0 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb, 1);
+      uint32_t t1 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb + 1 < kHashBits ? bb + 1 : bb, 1);
+      asm volatile("" : "+v"(t0), "+v"(t1));
+      const uint64_t m0 = ballot(t0 != 0u);
+      const uint64_t m1 = ballot(t1 != 0u);
+      // acc & ~(t ^ m) in one v_bitop3 per half (truth table 0x90)
+      lo = __builtin_amdgcn_bitop3_b32(lo, t0, (uint32_t)m0, 0x90);
+      hi = __builtin_amdgcn_bitop3_b32(hi, t0, (uint32_t)(m0 >> 32), 0x90);
+      if (bb + 1 < kHashBits) {
+        lo = __builtin_amdgcn_bitop3_b32(lo, t1, (uint32_t)m1, 0x90);
+        hi = __builtin_amdgcn_bitop3_b32(hi, t1, (uint32_t)(m1 >> 32), 0x90);
+      }
+    }
+    return (((uint64_t)hi << 32) | lo) & vm;
+  }
+};
+
+// BinGroup: two LDS bins per slot, slot & 127 and slot >> 7, each holding a
+// 64-bit lane mask that the chunk's valid lanes OR themselves into
+// (ds_or_b64).  Lanes found in both of my bins agree on every hash bit, so the
+// intersection is exactly my group.  Two atomics, two reads and two clears
+// (LDS runs one wave's ops in order) and a few VALU, in place of 13 ballots
+// and ~45 VALU; 1.5 KiB of LDS per wave, all zero between chunks.
+struct BinGroup {
+  uint64_t* b;
+  static constexpr uint32_t kBytes = (128u + 64u) * 8u;
+  __device__ __forceinline__ uint64_t same(uint32_t h, bool valid, uint64_t) const {
+    uint64_t* b0 = b + (h & 127u);
+    uint64_t* b1 = b + 128u + (h >> 7);
+    asm volatile("" ::: "memory");
+    if (valid) {
+      const uint64_t me = 1ull << lane_id();
+      __hip_atomic_fetch_or(b0, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_or(b1, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    asm volatile("" ::: "memory");
+    const uint64_t s = __hip_atomic_load(b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
+                       __hip_atomic_load(b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    __hip_atomic_store(b0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(b1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return s;
+  }
+};
+
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
 // points), like the reference.
-template <bool kWide, bool kGuard, class Src, class Tab>
-__device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const Tab& tab,
+template <bool kWide, bool kGuard, class Src, class Tab, class Grp>
+__device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const Tab& tab, const Grp& grp,
                                               uint8_t* __restrict__ out, int out_cap, int cap) {
-  constexpr int kHashBits = kWide ? 12 : 13;
   const uint32_t lane = lane_id();
   int op = 0;
   uint32_t anchor = 0;
@@ -263,32 +323,7 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         const uint32_t told = tab.get(h);
         const uint64_t vm = ballot(valid);
         // lanes of this chunk whose iteration hashes to the same slot
-        // (bit-sliced match-any: 13 ballots)
-        uint32_t lo = ~0u, hi = ~0u;
-#ifdef KDB_ABL_NO_GROUP
-        lo = hi = 0u;
-#else
-#pragma unroll
-        for (int bb = 0; bb < kHashBits; bb += 2) {
-          // t = 0 or ~0 (one v_bfe_i32); the empty asm keeps the ballot on t
-          // itself instead of a second shift + compare of h.  Bits go in pairs
-          // so each ballot's SGPR write is not read by the very next VALU op
-          // (no s_nop wait states).
-          uint32_t t0 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb, 1);
-          uint32_t t1 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb + 1 < kHashBits ? bb + 1 : bb, 1);
-          asm volatile("" : "+v"(t0), "+v"(t1));
-          const uint64_t m0 = ballot(t0 != 0u);
-          const uint64_t m1 = ballot(t1 != 0u);
-          // acc & ~(t ^ m) in one v_bitop3 per half (truth table 0x90)
-          lo = __builtin_amdgcn_bitop3_b32(lo, t0, (uint32_t)m0, 0x90);
-          hi = __builtin_amdgcn_bitop3_b32(hi, t0, (uint32_t)(m0 >> 32), 0x90);
-          if (bb + 1 < kHashBits) {
-            lo = __builtin_amdgcn_bitop3_b32(lo, t1, (uint32_t)m1, 0x90);
-            hi = __builtin_amdgcn_bitop3_b32(hi, t1, (uint32_t)(m1 >> 32), 0x90);
-          }
-        }
-#endif
-        const uint64_t same = (((uint64_t)hi << 32) | lo) & vm;
+        const uint64_t same = grp.same(h, valid, vm);
         const uint64_t below = same & mask_lt(lane);
         uint32_t refk = told;
         if (below) {                                 // reference = the nearest earlier same-slot lane
@@ -458,7 +493,10 @@ __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint
 //   dst slot capacity = cap[v].
 // kFrame = true : CompressorLZ4::Compress per value; the slot must hold
 //   8 + compress_bound(S) bytes; frame_len[v] = frame bytes, ret[v] = 0 or -1.
-template <bool kFrame, bool kSmall>
+//
+// kBins (kSmall only): same-slot grouping through LDS bins (BinGroup, placed
+// after the value) instead of 13 ballots per search chunk.
+template <bool kFrame, bool kSmall, bool kBins>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
@@ -466,6 +504,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
     int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
     uint32_t cls, uint32_t nq) {
+  static_assert(kSmall || !kBins, "bins sit after the fixed 4 KiB value region");
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
@@ -478,8 +517,15 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   Tab tab;
   if constexpr (kSmall) tab = Table12{smem, smem + 8192u};
   else tab = Table<false>{tab16, 0u};
+  using Grp = typename std::conditional<kBins, BinGroup, BallotGroup<13>>::type;
+  Grp grp{};
+  if constexpr (kBins) grp.b = reinterpret_cast<uint64_t*>(smem + kTabBytes + 4096u);
   if (kSmall) {
     for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(smem)[i] = z4;
+  }
+  if (kBins) {
+    for (uint32_t i = lane; i < BinGroup::kBytes / 16u; i += 64u)
+      reinterpret_cast<uint4*>(smem + kTabBytes + 4096u)[i] = z4;
   }
   // register prefetch (kSmall): the next value's realigned 16-byte chunks
   uint4 pa[kPrefetch], pb[kPrefetch];
@@ -531,11 +577,11 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t bound = compress_bound(S);
     if (!kFrame) {
       const uint32_t cap = uni(dst_cap[v]);
-      const int r = cap < bound ? compress_block<false, true>(LdsSrc{s_in}, S, tab, o, (int)cap, (int)cap)
-                                : compress_block<false, false>(LdsSrc{s_in}, S, tab, o, (int)bound, (int)cap);
+      const int r = cap < bound ? compress_block<false, true>(LdsSrc{s_in}, S, tab, grp, o, (int)cap, (int)cap)
+                                : compress_block<false, false>(LdsSrc{s_in}, S, tab, grp, o, (int)bound, (int)cap);
       if (lane == 0) ret[v] = r;
     } else {
-      const int r = compress_block<false, false>(LdsSrc{s_in}, S, tab, o + 8, (int)bound, (int)bound);
+      const int r = compress_block<false, false>(LdsSrc{s_in}, S, tab, grp, o + 8, (int)bound, (int)bound);
       if (r <= 0) {                              // compressor.cc:31-34
         if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
       } else {
@@ -565,8 +611,9 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 }
 
 // LDS bytes a launch needs for values up to max_len bytes.
-size_t compress_lds_bytes(uint32_t max_len) {
-  if (max_len <= kSmallMax) return kTable12Bytes + kSmallMax;   // 16 KiB: 10 per CU
+size_t compress_lds_bytes(uint32_t max_len, bool bins) {
+  // 16 KiB: 10 per CU; with the grouping bins 17.5 KiB: 9 per CU
+  if (max_len <= kSmallMax) return kTable12Bytes + kSmallMax + (bins ? BinGroup::kBytes : 0u);
   return kTableBytes + (((size_t)max_len + 15u) & ~(size_t)15u);
 }
 
@@ -591,6 +638,7 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   Tab tab;
   if constexpr (kWide) tab = Table32{tab32};
   else tab = Table<false>{reinterpret_cast<uint16_t*>(tab32), 0u};
+  const BallotGroup<kWide ? 12 : 13> grp{};
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
@@ -615,11 +663,12 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
         const uint32_t cap = uni(dst_cap[v]);
         int r = 0;
         if (bound != 0)
-          r = cap < bound ? compress_block<kWide, true>(GlobalSrc{g}, S, tab, o, (int)cap, (int)cap)
-                          : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o, (int)bound, (int)cap);
+          r = cap < bound ? compress_block<kWide, true>(GlobalSrc{g}, S, tab, grp, o, (int)cap, (int)cap)
+                          : compress_block<kWide, false>(GlobalSrc{g}, S, tab, grp, o, (int)bound, (int)cap);
         if (lane == 0) ret[v] = r;
       } else {
-        const int r = bound == 0 ? 0 : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o + 8, (int)bound, (int)bound);
+        const int r =
+            bound == 0 ? 0 : compress_block<kWide, false>(GlobalSrc{g}, S, tab, grp, o + 8, (int)bound, (int)bound);
         if (r <= 0) {                                             // compressor.cc:31-34
           if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
         } else {
@@ -664,12 +713,12 @@ __global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n
   }
 }
 
-template <bool F, bool Sm>
+template <bool F, bool Sm, bool Bn = false>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0) {
-  auto kern = lz4_compress_kernel<F, Sm>;
+  auto kern = lz4_compress_kernel<F, Sm, Bn>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
   if (e != hipSuccess) return e;
@@ -747,14 +796,25 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     if (e != hipSuccess) return e;
   }
   {
-    size_t lds = compress_lds_bytes(kSmallMax);
+    // KDB_LZ4_GROUP=ballot: the 13-ballot grouping at 10 per CU (A/B diagnostic)
+    static const bool bins = [] {
+      const char* g = getenv("KDB_LZ4_GROUP");
+      return !(g && strcmp(g, "ballot") == 0);
+    }();
+    size_t lds = compress_lds_bytes(kSmallMax, bins);
 #ifdef KDB_ABL_OCC
     lds = 163840 / KDB_ABL_OCC;   // diagnostic: force KDB_ABL_OCC workgroups per CU
 #endif
-    e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                       frame_len, ret, census, 0)
-              : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                        frame_len, ret, census, 0);
+    if (bins)
+      e = frame ? launch_one<true, true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off,
+                                               dst_cap, frame_len, ret, census, 0)
+                : launch_one<false, true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off,
+                                                dst_cap, frame_len, ret, census, 0);
+    else
+      e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                         frame_len, ret, census, 0)
+                : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                          frame_len, ret, census, 0);
     if (e != hipSuccess) return e;
   }
   // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
@@ -762,7 +822,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
   if (max_len > kSmallMax && mid_split > kSmallMax) {
     const uint32_t hi = min(min(max_len, mid_split), k64KLimit - 1u);
-    const size_t lds = compress_lds_bytes(hi);
+    const size_t lds = compress_lds_bytes(hi, false);
     e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
                                         dst_cap, frame_len, ret, census, 1)
               : launch_one<false, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
