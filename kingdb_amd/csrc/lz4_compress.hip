@@ -321,7 +321,8 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         if (kb == 0 && t0 && lane == 0) tab.put(hashp<kWide>(sm2), s - 3u);
         const uint32_t h = hashp<kWide>(seq);
         const uint32_t told = tab.get(h);
-        const uint64_t vm = ballot(valid);
+        const uint64_t vm = __builtin_amdgcn_uicmp(pk + (kb == 0 ? 1u : search_step(k)), mflimit, 37 /*ULE*/) |
+                            (kb == 0 ? (uint64_t)t0 : 0ull);   // = ballot(valid)
         // lanes of this chunk whose iteration hashes to the same slot
         const uint64_t same = grp.same(h, valid, vm);
         const uint64_t below = same & mask_lt(lane);
@@ -331,9 +332,11 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
           refk = kb == 0 ? s - t0 + jb : search_pos<kWide>(s, kb + jb - t0);
         }
         // byU32 adds the distance check (lz4.cc:526, 614); byU16 sizes never need it
-        const bool match = valid && (!kWide || refk + kMaxDistance >= pk) &&
-                           RD32(min(refk, last4)) == seq;   // lz4.cc:527, 610-616
-        const uint64_t mm = ballot(match);
+        // the lanes whose reference matches (lz4.cc:527, 610-616), as a
+        // compare straight into a lane mask (a ballot of a bool would be
+        // materialised in a VGPR and compared again)
+        uint64_t mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm;
+        if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
           const uint64_t later = same & ~mask_le(lane) & mask_le(ks);
@@ -506,7 +509,12 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     uint32_t cls, uint32_t nq) {
   static_assert(kSmall || !kBins, "bins sit after the fixed 4 KiB value region");
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  // kSmall: a fixed LDS layout, so every LDS address is a constant offset (a
+  // dynamic allocation's base costs a v_add per address)
+  constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u + (kBins ? BinGroup::kBytes : 0u) : 16u;
+  __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
+  uint8_t* const smem = kSmall ? smem_s : smem_d;
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
   constexpr uint32_t kTabBytes = kSmall ? kTable12Bytes : kTableBytes;
@@ -623,7 +631,7 @@ size_t compress_lds_bytes(uint32_t max_len, bool bins) {
 // 1 MB (util/options.h:171), so whole parts land here.  The value is read in
 // place from global memory (L2), the 16 KiB table lives in LDS; one wave per
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
-template <bool kFrame, bool kWide>
+template <bool kFrame, bool kWide, bool kBins>
 __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
@@ -632,13 +640,19 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     const uint32_t* __restrict__ census, uint32_t cls) {
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
   __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
+  __shared__ __attribute__((aligned(16))) uint64_t bins_s[kBins ? BinGroup::kBytes / 8u : 1u];
   const uint32_t lane = lane_id();
   // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
   using Tab = typename std::conditional<kWide, Table32, Table<false>>::type;
   Tab tab;
   if constexpr (kWide) tab = Table32{tab32};
   else tab = Table<false>{reinterpret_cast<uint16_t*>(tab32), 0u};
-  const BallotGroup<kWide ? 12 : 13> grp{};
+  using Grp = typename std::conditional<kBins, BinGroup, BallotGroup<kWide ? 12 : 13>>::type;
+  Grp grp{};
+  if constexpr (kBins) {
+    grp.b = bins_s;
+    for (uint32_t i = lane; i < BinGroup::kBytes / 8u; i += 64u) bins_s[i] = 0ull;
+  }
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
@@ -734,7 +748,12 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                              uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst, const uint64_t* dst_off,
                              const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret,
                              const uint32_t* census = nullptr, uint32_t cls = 0) {
-  auto kern = lz4_compress_big_kernel<F, W>;
+  // KDB_LZ4_BIGGROUP=bins|ballot: same-slot grouping of the in-place kernels
+  static const bool bins = [] {
+    const char* g = getenv("KDB_LZ4_BIGGROUP");
+    return g && strcmp(g, "bins") == 0;
+  }();
+  auto kern = bins ? lz4_compress_big_kernel<F, W, true> : lz4_compress_big_kernel<F, W, false>;
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
   if (e != hipSuccess) return e;
@@ -801,10 +820,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
       const char* g = getenv("KDB_LZ4_GROUP");
       return !(g && strcmp(g, "ballot") == 0);
     }();
-    size_t lds = compress_lds_bytes(kSmallMax, bins);
-#ifdef KDB_ABL_OCC
-    lds = 163840 / KDB_ABL_OCC;   // diagnostic: force KDB_ABL_OCC workgroups per CU
-#endif
+    const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax, bins) bytes)
     if (bins)
       e = frame ? launch_one<true, true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off,
                                                dst_cap, frame_len, ret, census, 0)
