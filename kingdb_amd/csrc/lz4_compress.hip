@@ -280,16 +280,19 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
     const uint32_t last4 = S - 4u;                          // highest position a u32 read may start
     // lz4.cc:486: put(0) stores position 0 -- what an empty slot already reads as.
     //
-    // The "test next position" step after a match (lz4.cc:600-618: get(ip),
-    // put(ip), compare; the distance check there always holds for byU16
-    // sizes) is a search iteration at ip without the skip counter, followed --
-    // when it fails -- by a fresh search from ip+1 whose first 65 iterations
-    // advance by 1.  So it runs as lane 0 of the next search chunk: positions
-    // ip, ip+1, ..., ip+63, lane 0 valid unconditionally (ip <= mflimit was
-    // checked), lanes >= 1 being search iterations 0..62.  A lane-0 match is
+    // After a match ending at ip the reference puts ip-2 (lz4.cc:600), then
+    // tests ip (lz4.cc:603-618: get(ip), put(ip), compare; the distance check
+    // there always holds for byU16 sizes) -- a search iteration at ip without
+    // the skip counter -- and, when that fails, searches afresh from ip+1,
+    // whose first 65 iterations advance by 1.  So all of it is the next
+    // search chunk, positions ip-2 .. ip+60 ("lead" chunk): lane 0 = ip-2,
+    // put only (never a match; later same-slot lanes take it as their
+    // reference like any earlier lane); lane 1 = ip-1, dead (no get, no put);
+    // lane 2 = ip, the test, valid unconditionally (ip <= mflimit was
+    // checked); lanes >= 3 = search iterations 0..60.  A lane-2 match is
     // _next_match: no catch-up, no literals.
     uint32_t s = 1;                                         // lz4.cc:487
-    uint32_t t0 = 0;                                        // 1: lane 0 of the first chunk is the test
+    uint32_t t0 = 0;                                        // 1: the first chunk is a lead chunk
     uint32_t pf = 0;                                        // GlobalSrc: the frontier prefetch in flight
     for (;;) {
       pf = src.prefetch(s, S, pf);
@@ -298,15 +301,16 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
       bool found = false, catchup = true;
 #pragma unroll 1
       for (uint32_t kb = 0;; kb += 64u) {
-        // positions: step(k) = 1 for k <= 64, so the first chunk is s-t0+lane
-        const uint32_t k = kb + lane - t0;
-        const uint32_t pk = kb == 0 ? s - t0 + lane : search_pos<kWide>(s, k);
-        const bool valid = (kb == 0 && lane < t0) || pk + (kb == 0 ? 1u : search_step(k)) <= mflimit;  // lz4.cc:510
+        // positions: step(k) = 1 for k <= 64, so the first chunk is s-o3+lane
+        const bool lead = kb == 0 && t0 != 0;
+        const uint32_t o3 = 3u * t0;
+        const uint32_t k = kb + lane - o3;
+        const uint32_t pk = kb == 0 ? s - o3 + lane : search_pos<kWide>(s, k);
+        // valid lanes (lz4.cc:510), as a compare straight into a lane mask
+        uint64_t vm = __builtin_amdgcn_uicmp(pk + (kb == 0 ? 1u : search_step(k)), mflimit, 37 /*ULE*/);
+        if (lead) vm = (vm | 5ull) & ~2ull;
+        const bool valid = (vm >> lane) & 1ull;
         const uint32_t seq = RD32(min(pk, last4));
-        // lz4.cc:600 put(ip-2) of the previous sequence (ip = s-1): its read
-        // shares the round trip of the chunk's reads; the store precedes the
-        // chunk's table reads (in-order LDS)
-        const uint32_t sm2 = RD32(max(s, 3u) - 3u);
         if (!kGuard) {                               // the pending sequence
           const uint32_t j = lane;
           const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
@@ -318,24 +322,21 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
           if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
           pe_total = 0;
         }
-        if (kb == 0 && t0 && lane == 0) tab.put(hashp<kWide>(sm2), s - 3u);
         const uint32_t h = hashp<kWide>(seq);
         const uint32_t told = tab.get(h);
-        const uint64_t vm = __builtin_amdgcn_uicmp(pk + (kb == 0 ? 1u : search_step(k)), mflimit, 37 /*ULE*/) |
-                            (kb == 0 ? (uint64_t)t0 : 0ull);   // = ballot(valid)
         // lanes of this chunk whose iteration hashes to the same slot
         const uint64_t same = grp.same(h, valid, vm);
         const uint64_t below = same & mask_lt(lane);
         uint32_t refk = told;
         if (below) {                                 // reference = the nearest earlier same-slot lane
           const uint32_t jb = 63u - (uint32_t)__builtin_clzll(below);
-          refk = kb == 0 ? s - t0 + jb : search_pos<kWide>(s, kb + jb - t0);
+          refk = kb == 0 ? s - o3 + jb : search_pos<kWide>(s, kb + jb - o3);
         }
         // byU32 adds the distance check (lz4.cc:526, 614); byU16 sizes never need it
         // the lanes whose reference matches (lz4.cc:527, 610-616), as a
         // compare straight into a lane mask (a ballot of a bool would be
         // materialised in a VGPR and compared again)
-        uint64_t mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm;
+        uint64_t mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm & (lead ? ~1ull : ~0ull);
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
@@ -343,12 +344,12 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
           if (valid && lane <= ks && later == 0) tab.put(h, pk);   // lz4.cc:526, 608
           ip = readlane(pk, ks);
           ref = readlane(refk, ks);
-          catchup = !(kb == 0 && ks < t0);
+          catchup = !(lead && ks == 2u);
           found = true;
           break;
         }
-        if (vm != ~0ull) break;              // ran past mflimit: last literals
-        if ((same & ~mask_le(lane)) == 0) tab.put(h, pk);
+        if ((vm | (lead ? 2ull : 0ull)) != ~0ull) break;   // ran past mflimit: last literals
+        if (valid && (same & ~mask_le(lane)) == 0) tab.put(h, pk);
       }
       if (!found) break;
 
