@@ -157,24 +157,33 @@ struct GlobalSrc {
 // which the block never exceeds.
 //
 // Writes the encoding of one sequence at out[pos .. pos+total): token, the
-// literal-length run (nl bytes of 255 + remL, present iff lit >= 15), the
+// literal-length run (nl1 bytes: 255s then remL; none iff lit < 15), the
 // literals in[anchor .. anchor+lit), and -- when has_match -- the offset (LE16)
-// and the match-length run (nm bytes of 255 + remM, present iff long_ml).
+// and the match-length run (nm1 bytes: 255s then remM; none iff ml < 15).
 // One global_store_byte per 64 bytes.  Returns total.
+//
+// Run lengths: a run of n >= 15 is (n-15)/255 bytes of 255 and one of
+// (n-15) % 255 (lz4.cc:539-545, 582-590), i.e. nl1 = (n+240)/255 bytes ending
+// in n+240-255*nl1; for n < 15 the same formulas give nl1 = 0.
+__device__ __forceinline__ uint32_t run_bytes(uint32_t n) { return (n + 240u) / 255u; }
+__device__ __forceinline__ uint32_t run_last(uint32_t n, uint32_t nb) { return n + 240u - 255u * nb; }
+
 template <bool kGuard, class Src>
 __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, int pos, uint32_t token,
-                                        uint32_t lit, uint32_t nl, uint32_t remL, const Src& src,
+                                        uint32_t lit, uint32_t nl1, uint32_t remL, const Src& src,
                                         uint32_t S, uint32_t anchor, bool has_match, uint32_t off,
-                                        bool long_ml, uint32_t nm, uint32_t remM) {
+                                        uint32_t nm1, uint32_t remM) {
   const uint32_t lane = lane_id();
-  const uint32_t a = 1u + (lit >= kRunMask ? nl + 1u : 0u);      // first literal byte
+  const uint32_t a = 1u + nl1;                                     // first literal byte
   const uint32_t b = a + lit;                                      // offset low byte
-  const uint32_t total = has_match ? b + 2u + (long_ml ? nm + 1u : 0u) : b;
+  const uint32_t total = has_match ? b + 2u + nm1 : b;
 #ifndef KDB_ABL_NO_EMIT
   // One pass per 64 bytes; every byte class is a compare-select: token,
   // 255-run bytes, remL, literals (one LDS byte read), offset, 255-run, remM.
-  const uint32_t remL_at = lit >= kRunMask ? a - 1u : 0xFFFFFFFFu;     // 0 is the token
-  const uint32_t remM_at = long_ml ? total - 1u : 0xFFFFFFFFu;
+  // Without a run its "last byte" index falls on a byte of higher precedence
+  // (the token, resp. the offset's high byte or a literal).
+  const uint32_t remL_at = a - 1u;
+  const uint32_t remM_at = total - 1u;
   const int lbase = (int)anchor - (int)a;
 #pragma clang loop unroll(disable)
   for (uint32_t i = 0; i < total; i += 64u) {
@@ -407,31 +416,29 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
         if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
       }
-      const uint32_t token = ((lit >= kRunMask ? kRunMask : lit) << 4) | (long_ml ? kMlMask : ml);
-      const uint32_t nl = lit >= kRunMask ? (lit - kRunMask) / 255u : 0u;
-      const uint32_t nm = long_ml ? (ml - kMlMask) / 255u : 0u;
-      const uint32_t remL = lit - kRunMask - 255u * nl, remM = ml - kMlMask - 255u * nm;
-      const uint32_t ea = 1u + (lit >= kRunMask ? nl + 1u : 0u);
-      const uint32_t etot = ea + lit + 2u + (long_ml ? nm + 1u : 0u);
+      const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
+      const uint32_t nl1 = run_bytes(lit), nm1 = run_bytes(ml);
+      const uint32_t remL = run_last(lit, nl1), remM = run_last(ml, nm1);   // < 255 each
+      const uint32_t ea = 1u + nl1;
+      const uint32_t etot = ea + lit + 2u + nm1;
       if (!kGuard && etot <= 64u) {
         pe_pos = op;
         pe_lbase = (int)anchor - (int)ea;
         pe_a = ea;
         pe_b = ea + lit;
         pe_total = etot;
-        pe_w0 = token | ((lit >= kRunMask ? remL : 0u) << 8) | ((long_ml ? remM : 0u) << 16);
+        pe_w0 = token | (remL << 8) | (remM << 16);
         pe_w1 = ip - ref;
         op += (int)etot;
       } else {
-        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl, remL, src, S, anchor, true, ip - ref, long_ml,
-                               nm, remM);
+        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl1, remL, src, S, anchor, true, ip - ref, nm1, remM);
       }
       ip = ip_end;
       anchor = ip;
       if (ip > mflimit) goto last_literals;                      // lz4.cc:597
 
-      // the table fill of ip-2 (lz4.cc:600) and the test of ip (lane 0) run
-      // with the next chunk
+      // the table fill of ip-2 (lz4.cc:600) and the test of ip run as the
+      // next (lead) chunk
       s = ip + 1u;                                              // lz4.cc:623
       t0 = 1u;
     }
@@ -451,10 +458,9 @@ last_literals:
   {  // lz4.cc:627-637
     const uint32_t run = S - anchor;
     if (kGuard && op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
-    const uint32_t nl = run >= kRunMask ? (run - kRunMask) / 255u : 0u;
-    const uint32_t tok = (run >= kRunMask ? kRunMask : run) << 4;
-    op += emit_seq<kGuard>(out, out_cap, op, tok, run, nl, run - kRunMask - 255u * nl, src, S, anchor, false, 0u,
-                           false, 0u, 0u);
+    const uint32_t nl1 = run_bytes(run);
+    op += emit_seq<kGuard>(out, out_cap, op, min(run, kRunMask) << 4, run, nl1, run_last(run, nl1), src, S, anchor,
+                           false, 0u, 0u, 0u);
   }
 #undef RD32
   return op;
