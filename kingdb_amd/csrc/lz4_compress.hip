@@ -375,8 +375,9 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         const uint32_t a0 = src.u8(cl ? ip - 1u - lane : 0u), b0 = src.u8(cl ? ref - 1u - lane : 0u);
         const uint32_t a1 = src.u8(ml_in ? ip + kMinMatch + lane : 0u);
         const uint32_t b1 = src.u8(ml_in ? ref + kMinMatch + lane : 0u);
-        c = first_zero(ballot(cl && a0 == b0));      // <= lim: lanes past it vote false
-        ml = first_zero(ballot(ml_in && a1 == b1));  // <= rem
+        // compares straight into lane masks; lanes past lim / rem vote false
+        c = first_zero(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & (lim >= 64u ? ~0ull : mask_lt(lim)));
+        ml = first_zero(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & (rem >= 64u ? ~0ull : mask_lt(rem)));
         if (c == 64u) {
 #pragma unroll 1
           for (;;) {
