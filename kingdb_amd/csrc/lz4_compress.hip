@@ -500,6 +500,16 @@ __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint
   for (uint32_t c = lane_id(); c < chunks; c += 64u) l[c] = head ? funnel16(base[c], base[c + 1u], head) : base[c];
 }
 
+// Per-value metadata read through the scalar cache (s_load, counted by
+// lgkmcnt): a vector load would be counted by vmcnt behind the next value's
+// prefetch loads and the previous value's byte stores, and waiting for it
+// (vmcnt(0): the counts are not static) exposed the whole prefetch latency
+// at every value.
+template <class T>
+__device__ __forceinline__ T sload(const T* p, uint32_t i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
 // kFrame = false: LZ4_compress_limitedOutput per value; ret[v] = size or 0,
 //   dst slot capacity = cap[v].
 // kFrame = true : CompressorLZ4::Compress per value; the slot must hold
@@ -547,13 +557,13 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   uint4 pa[kPrefetch], pb[kPrefetch];
   uint32_t p_head = 0, p_chunks = 0;
   WorkQueue wq = WorkQueue::make(work, n, batch, nq);
-  uint32_t v = wq.next();
+  uint32_t v = uni(wq.next());
   auto prefetch = [&](uint32_t w) {
     if (w < n) {
-      const uint8_t* gp = src + src_off[w];
+      const uint8_t* gp = src + sload(src_off, w);
       p_head = uni((uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u));
       const uint4* base = reinterpret_cast<const uint4*>(gp - p_head);
-      const uint32_t len = uni(src_len[w]);
+      const uint32_t len = sload(src_len, w);
       p_chunks = (len >= min_len && len <= in_cap) ? (len + 15u) >> 4 : 0u;   // other launches' values: none
 #pragma unroll
       for (uint32_t i = 0; i < kPrefetch; ++i) {
@@ -566,10 +576,10 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   if (kSmall) prefetch(v);
 
   while (v < n) {
-    const uint32_t vn = wq.next();         // the next value, one ahead
-    const uint32_t S = uni(src_len[v]);
-    const uint8_t* g = src + src_off[v];
-    uint8_t* o = dst + dst_off[v];
+    const uint32_t vn = uni(wq.next());    // the next value, one ahead
+    const uint32_t S = sload(src_len, v);
+    const uint8_t* g = src + sload(src_off, v);
+    uint8_t* o = dst + sload(dst_off, v);
     if (S < min_len || S > in_cap) {             // another size class's launch owns it
       if (kSmall) prefetch(vn);
       v = vn;
