@@ -95,17 +95,21 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       if (((far_ip - ip) | (far_op - op) | (45 - xl)) >= 0) {
         const int ls = ip + 1 + lx;
         const int opl = op + lit;
-        const uint32_t v = in[ls + (int)lane];
-        const int e = (int)readlane(v, (uint32_t)lit + 2u);
-        const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
+        // lane i holds the block's 4 bytes from ls + i: byte 0 is literal i,
+        // and one readlane gives the offset + match-length byte, another the
+        // next token and the byte after it
+        const uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
+        const uint32_t w = readlane(v, (uint32_t)lit);
+        const int e = (int)((w >> 16) & 0xffu);
+        const int off = (int)(w & 0xffffu);
         const int mx = (mn + 1) >> 4;                             // a match-length byte follows
         const int xm = e & -mx;
         const int mlen = mn + xm + (int)kMinMatch;
         if (((opl - off) | (254 - xm)) >= 0) {                    // ref >= 0; one match-length byte
           out[op + (int)lane] = (uint8_t)v;        // lz4.cc:947 (lanes past lit: not-yet-produced output)
           const uint32_t nt = (uint32_t)(lit + 2 + mx);             // next token's lane (<= 63)
-          q = readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8);
-          have_q = (int)(63u - nt);             // > 0: the byte after the token was in the load too
+          q = readlane(v, nt);
+          have_q = 1;
           ip = ls + lit + 2 + mx;
           const int ref = opl - off;
           asm volatile("" ::: "memory");
