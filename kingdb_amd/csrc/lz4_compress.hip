@@ -242,15 +242,14 @@ struct BallotGroup {
 struct BinGroup {
   uint64_t* b;
   static constexpr uint32_t kBytes = (128u + 64u) * 8u;
-  __device__ __forceinline__ uint64_t same(uint32_t h, bool valid, uint64_t) const {
+  __device__ __forceinline__ uint64_t same(uint32_t h, bool, uint64_t vm) const {
     uint64_t* b0 = b + (h & 127u);
     uint64_t* b1 = b + 128u + (h >> 7);
     asm volatile("" ::: "memory");
-    if (valid) {
-      const uint64_t me = 1ull << lane_id();
-      __hip_atomic_fetch_or(b0, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_or(b1, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    // every lane ORs (its bit if valid, else 0): no exec-mask save/restore
+    const uint64_t me = (1ull << lane_id()) & vm;
+    __hip_atomic_fetch_or(b0, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_or(b1, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     asm volatile("" ::: "memory");
     const uint64_t s = __hip_atomic_load(b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
                        __hip_atomic_load(b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
