@@ -561,14 +561,20 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     if (w < n) {
       const uint8_t* gp = src + sload(src_off, w);
       p_head = uni((uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u));
-      const uint4* base = reinterpret_cast<const uint4*>(gp - p_head);
+      const uint4* base = reinterpret_cast<const uint4*>(__builtin_assume_aligned(gp - p_head, 16));
       const uint32_t len = sload(src_len, w);
       p_chunks = (len >= min_len && len <= in_cap) ? (len + 15u) >> 4 : 0u;   // other launches' values: none
+      // whole-wave 16-byte loads (no per-lane exec masks, so global_load_dwordx4),
+      // indices clamped to the last aligned chunk holding value bytes; lanes
+      // past p_chunks load data the staging ignores
+      if (p_chunks) {
+        const uint32_t last = (p_head + len - 1u) >> 4;
 #pragma unroll
-      for (uint32_t i = 0; i < kPrefetch; ++i) {
-        const uint32_t c = lane + 64u * i;
-        pa[i] = c < p_chunks ? base[c] : z4;
-        pb[i] = (p_head && c < p_chunks) ? base[c + 1u] : z4;
+        for (uint32_t i = 0; i < kPrefetch; ++i) {
+          const uint32_t c = lane + 64u * i;
+          pa[i] = base[min(c, last)];
+          pb[i] = base[min(c + 1u, last)];
+        }
       }
     }
   };
