@@ -442,6 +442,13 @@ def main() -> None:
     from kingdb_amd import lz4 as L
     from kingdb_amd.shard import g1_first_piece, gather_ranks, max_over_ranks
 
+    # One rank per GPU.  More ranks than GPUs (a rehearsal of the N > 1 path on
+    # a 1-GPU box) share devices round-robin; on a full node this is identity.
+    n_dev = torch.cuda.device_count()
+    if n_dev > 0 and local >= n_dev:
+        print(f"warning: LOCAL_RANK={local} >= {n_dev} visible GPU(s): rank shares GPU "
+              f"{local % n_dev} (rehearsal only)", file=sys.stderr)
+        local = local % n_dev
     K.set_device(local)
     torch_sync = torch.cuda.is_available()
     if torch_sync:
