@@ -142,4 +142,9 @@ uint32_t claim_batch(uint32_t n, uint32_t grid) {
   return (uint32_t)b;
 }
 
+uint32_t env_prio() {
+  const char* e = getenv("KDB_LZ4_BIGPRIO");
+  return e && *e && *e != '0' ? 1u : 0u;
+}
+
 }  // namespace kdb_lz4

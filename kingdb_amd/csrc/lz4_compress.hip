@@ -660,8 +660,11 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    const uint32_t* __restrict__ census, uint32_t cls) {
+    const uint32_t* __restrict__ census, uint32_t cls, uint32_t prio) {
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
+  // the big class is a mixed batch's critical path: its waves win issue
+  // arbitration over the small classes' waves that fill the GPU beside them
+  if (prio) __builtin_amdgcn_s_setprio(2);
   __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
   __shared__ __attribute__((aligned(16))) uint64_t bins_s[kBins ? BinGroup::kBytes / 8u : 1u];
   const uint32_t lane = lane_id();
@@ -777,13 +780,14 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
     return g && strcmp(g, "bins") == 0;
   }();
   auto kern = bins ? lz4_compress_big_kernel<F, W, true> : lz4_compress_big_kernel<F, W, false>;
+  static const uint32_t prio = env_prio();
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
   if (e != hipSuccess) return e;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
   const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
-                     dst_cap, frame_len, ret, work, batch, census, cls);
+                     dst_cap, frame_len, ret, work, batch, census, cls, prio);
   return hipGetLastError();
 }
 

@@ -588,8 +588,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    uint32_t prio) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (prio) __builtin_amdgcn_s_setprio(2);     // a mixed batch's critical path (see launch_compress)
   const uint32_t lane = lane_id();
   uint8_t* ring = smem;
   uint8_t* iring = smem + kORing;
@@ -703,6 +705,7 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                              uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst, const uint64_t* dst_off,
                              const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   auto kern = lz4_decompress_big_kernel<F, R>;
+  static const uint32_t prio = env_prio();
   uint32_t* work = nullptr;
   hipError_t e = work_counter(st, &work);
   if (e != hipSuccess) return e;
@@ -710,7 +713,7 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
-                     dst_off, out_cap, target, out_len, ret, work, batch);
+                     dst_off, out_cap, target, out_len, ret, work, batch, prio);
   return hipGetLastError();
 }
 

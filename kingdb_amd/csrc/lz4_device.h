@@ -161,5 +161,8 @@ uint32_t work_queues(uint32_t max_len);
 // fork_end makes st wait for aux (KDB_LZ4_NOFORK=1: aux == st)
 hipError_t fork_begin(hipStream_t st, hipStream_t* aux);
 hipError_t fork_end(hipStream_t st, hipStream_t aux);
+// wave priority of the big-value (in-place / ring) class launches, whose
+// values are a mixed batch's critical path (KDB_LZ4_BIGPRIO, default 0)
+uint32_t env_prio();
 
 }  // namespace kdb_lz4
