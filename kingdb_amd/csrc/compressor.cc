@@ -3,6 +3,11 @@
 // Control flow and Status behaviour follow /root/reference/algorithm/compressor.cc
 // line by line (cited per method); every LZ4 block is produced / decoded by the
 // HIP kernels behind include/kdb_lz4.h.
+//
+// Built two ways: standalone (against kdb_types.h's mirrors, e.g. tests/cpp),
+// or inside KingDB with -DKDB_LZ4_IN_KINGDB and the shadow include directory
+// kingdb_amd/kingdb_include ahead of KingDB's root (oracle/Makefile `kingdb`,
+// INTEGRATION.md level 2).
 #include "compressor.h"
 
 #include <cstring>
@@ -10,7 +15,7 @@
 
 #include "kdb_lz4.h"
 
-namespace kdb {
+KDB_LZ4_NS_OPEN
 
 namespace {
 inline void put_u32le(char* p, uint32_t v) {
@@ -208,18 +213,47 @@ Status CompressorLZ4::UncompressByteArray(ByteArray& value, bool do_checksum_ver
 
 // ---------------------------------------------------------------- batches
 namespace {
-struct Pinned {
-  void* p = nullptr;
-  ~Pinned() {
-    if (p) kdb_lz4_host_free(p);
+// Per-thread staging of the batch methods: pinned host and device buffers
+// that grow on demand and are kept across calls (an allocation per call cost
+// milliseconds: hipHostMalloc/hipMalloc of the whole batch), plus a stream.
+struct BatchStaging {
+  void* host = nullptr;
+  void* dev = nullptr;
+  void* stream = nullptr;
+  uint64_t cap = 0;
+  int device = -1;
+  ~BatchStaging() { release(); }
+  void release() {
+    if (host) kdb_lz4_host_free(host);
+    if (dev) kdb_lz4_free(dev);
+    if (stream) kdb_lz4_stream_destroy(stream);
+    host = dev = stream = nullptr;
+    cap = 0;
+  }
+  bool reserve(uint64_t bytes) {
+    int d = 0;
+    if (kdb_lz4_get_device(&d) != KDB_LZ4_OK) return false;
+    if (d != device) {           // buffers and stream belong to one device
+      release();
+      device = d;
+    }
+    if (!stream && kdb_lz4_stream_create(&stream) != KDB_LZ4_OK) return false;
+    if (bytes <= cap) return true;
+    uint64_t want = cap ? cap : (1ull << 20);
+    while (want < bytes) want *= 2;
+    if (host) kdb_lz4_host_free(host);
+    if (dev) kdb_lz4_free(dev);
+    host = dev = nullptr;
+    cap = 0;
+    if (kdb_lz4_host_alloc(&host, want) != KDB_LZ4_OK || kdb_lz4_malloc(&dev, want) != KDB_LZ4_OK) return false;
+    cap = want;
+    return true;
   }
 };
-struct Dev {
-  void* p = nullptr;
-  ~Dev() {
-    if (p) kdb_lz4_free(p);
-  }
-};
+BatchStaging& batch_staging() {
+  thread_local BatchStaging s;
+  return s;
+}
 inline uint64_t a16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 }  // namespace
 
@@ -236,11 +270,9 @@ Status CompressorLZ4::CompressFrames(uint32_t n, char* const* raw_in, const uint
     dst_bytes += a16(kdb_lz4_frame_bound((uint32_t)size_raw_in[i]));
     if (size_raw_in[i] > max_len) max_len = (uint32_t)size_raw_in[i];
   }
-  const uint64_t total = meta + src_bytes + dst_bytes;
-  Pinned h;
-  Dev d;
-  if (kdb_lz4_host_alloc(&h.p, total) || kdb_lz4_malloc(&d.p, total)) return Status::IOError("GPU allocation failed");
-  char* hb = static_cast<char*>(h.p);
+  BatchStaging& b = batch_staging();
+  if (!b.reserve(meta + src_bytes + dst_bytes)) return Status::IOError("GPU allocation failed");
+  char* hb = static_cast<char*>(b.host);
   uint64_t* src_off = reinterpret_cast<uint64_t*>(hb);
   uint32_t* src_len = reinterpret_cast<uint32_t*>(hb + 8ull * n);
   uint64_t* dst_off = reinterpret_cast<uint64_t*>(hb + 12ull * n);
@@ -255,9 +287,8 @@ Status CompressorLZ4::CompressFrames(uint32_t n, char* const* raw_in, const uint
     dst_off[i] = dof;
     dof += a16(kdb_lz4_frame_bound((uint32_t)size_raw_in[i]));
   }
-  char* db = static_cast<char*>(d.p);
-  void* st = nullptr;
-  if (kdb_lz4_stream_create(&st)) return Status::IOError("stream");
+  char* db = static_cast<char*>(b.dev);
+  void* st = b.stream;
   int rc = kdb_lz4_memcpy_h2d(db, hb, meta + src_bytes, st);
   if (!rc)
     rc = kdb_lz4_compress_frames_batch(st, reinterpret_cast<uint8_t*>(db), reinterpret_cast<uint64_t*>(db),
@@ -268,11 +299,13 @@ Status CompressorLZ4::CompressFrames(uint32_t n, char* const* raw_in, const uint
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb, db, meta, st);
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb + meta + src_bytes, db + meta + src_bytes, dst_bytes, st);
   if (!rc) rc = kdb_lz4_stream_sync(st);
-  kdb_lz4_stream_destroy(st);
   if (rc) return Status::IOError("GPU compress batch failed");
   for (uint32_t i = 0; i < n; i++) {
     if (status[i] != 0) {
-      for (uint32_t j = 0; j < i; j++) delete[] frames[j];
+      for (uint32_t j = 0; j < i; j++) {
+        delete[] frames[j];
+        frames[j] = nullptr;
+      }
       return Status::IOError("LZ4_compress_limitedOutput() failed", std::to_string(i));
     }
     frames[i] = new char[frame_len[i]];
@@ -297,11 +330,9 @@ Status CompressorLZ4::UncompressFrames(uint32_t n, char* const* frames, const ui
     if (frame_avail[i] > max_in) max_in = (uint32_t)frame_avail[i];
     if (out_cap[i] > max_out) max_out = (uint32_t)out_cap[i];
   }
-  const uint64_t total = meta + src_bytes + dst_bytes;
-  Pinned h;
-  Dev d;
-  if (kdb_lz4_host_alloc(&h.p, total) || kdb_lz4_malloc(&d.p, total)) return Status::IOError("GPU allocation failed");
-  char* hb = static_cast<char*>(h.p);
+  BatchStaging& b = batch_staging();
+  if (!b.reserve(meta + src_bytes + dst_bytes)) return Status::IOError("GPU allocation failed");
+  char* hb = static_cast<char*>(b.host);
   uint64_t* src_off = reinterpret_cast<uint64_t*>(hb);
   uint32_t* avail = reinterpret_cast<uint32_t*>(hb + 8ull * n);
   uint64_t* dst_off = reinterpret_cast<uint64_t*>(hb + 12ull * n);
@@ -318,9 +349,8 @@ Status CompressorLZ4::UncompressFrames(uint32_t n, char* const* frames, const ui
     dst_cap[i] = (uint32_t)out_cap[i];
     dof += a16(out_cap[i]);
   }
-  char* db = static_cast<char*>(d.p);
-  void* st = nullptr;
-  if (kdb_lz4_stream_create(&st)) return Status::IOError("stream");
+  char* db = static_cast<char*>(b.dev);
+  void* st = b.stream;
   int rc = kdb_lz4_memcpy_h2d(db, hb, meta + src_bytes, st);
   if (!rc)
     rc = kdb_lz4_decompress_frames_batch(
@@ -331,7 +361,6 @@ Status CompressorLZ4::UncompressFrames(uint32_t n, char* const* frames, const ui
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb, db, meta, st);
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb + meta + src_bytes, db + meta + src_bytes, dst_bytes, st);
   if (!rc) rc = kdb_lz4_stream_sync(st);
-  kdb_lz4_stream_destroy(st);
   if (rc) return Status::IOError("GPU decompress batch failed");
   for (uint32_t i = 0; i < n; i++) {
     if (status[i] != 0) return Status::IOError("LZ4_decompress_safe_partial() failed", std::to_string(i));
@@ -341,4 +370,4 @@ Status CompressorLZ4::UncompressFrames(uint32_t n, char* const* frames, const ui
   return Status::OK();
 }
 
-}  // namespace kdb
+KDB_LZ4_NS_CLOSE  // namespace kdb

@@ -18,7 +18,20 @@
 
 #include "kdb_types.h"
 
-namespace kdb {
+// Outside KingDB the class sits in the inline namespace kdb::standalone with
+// the type mirrors (kdb_types.h); inside (KDB_LZ4_IN_KINGDB, set by
+// kingdb_amd/kingdb_include/algorithm/compressor.h and by the build of this
+// file for KingDB) it is kdb::CompressorLZ4 itself, the friend that
+// util/byte_array.h names.
+#ifdef KDB_LZ4_IN_KINGDB
+#define KDB_LZ4_NS_OPEN namespace kdb {
+#define KDB_LZ4_NS_CLOSE }
+#else
+#define KDB_LZ4_NS_OPEN namespace kdb { inline namespace standalone {
+#define KDB_LZ4_NS_CLOSE } }
+#endif
+
+KDB_LZ4_NS_OPEN
 
 // thread/threadstorage.h:23-46: one uint64_t per calling thread, default 0.
 class ThreadStorageLZ4 {
@@ -110,4 +123,4 @@ class CompressorLZ4 {
   bool crc_double_stream_ = true;
 };
 
-}  // namespace kdb
+KDB_LZ4_NS_CLOSE  // namespace kdb

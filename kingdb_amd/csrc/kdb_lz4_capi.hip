@@ -16,7 +16,7 @@
 
 namespace kdb_lz4 {
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
-                           const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
+                           const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret);
 hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
@@ -41,31 +41,52 @@ inline int hip_status(hipError_t e) {
 // Largest value the byU16 kernels take (lz4.cc:673: S < 65547).
 
 // Per-thread, per-device context of the scalar entry points.
+//
+// A scalar call is latency, not bandwidth: one value, one kernel, the caller
+// waiting.  Values whose class kernel touches each input byte once and writes
+// each output byte once (compress <= 8 KiB, decode of <= 8 KiB output: the
+// LDS-staged kernels) run ZERO-COPY: metadata, input and output live in one
+// pinned, coherent, device-mapped host buffer that the kernel reads and writes
+// over PCIe -- one launch and one stream sync per call, no DMA.  Larger values
+// (the in-place kernels read the input many times; the ring decoder reads
+// back its own output) are staged through device memory: one H2D copy, the
+// launch, one D2H copy of metadata + output, one sync.
 struct ScalarCtx {
   hipStream_t stream = nullptr;
-  uint8_t* dev = nullptr;     // [meta 64 B][in][out]
-  uint8_t* host = nullptr;    // pinned mirror
-  size_t cap = 0;
+  uint8_t* host = nullptr;    // pinned, coherent, mapped: [meta 64 B][in][out]
+  uint8_t* hdev = nullptr;    // its device address
+  size_t hcap = 0;
+  uint8_t* dev = nullptr;     // device staging for large values: [meta 64 B][out][in]
+  size_t dcap = 0;
   ~ScalarCtx() {
     if (dev) (void)hipFree(dev);
     if (host) (void)hipHostFree(host);
     if (stream) (void)hipStreamDestroy(stream);
   }
-  int reserve(size_t bytes) {
-    if (!stream) {
-      if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return KDB_LZ4_EHIP;
-    }
-    if (bytes <= cap) return KDB_LZ4_OK;
-    size_t want = cap ? cap : 1u << 16;
+  static size_t grow(size_t have, size_t bytes) {
+    size_t want = have ? have : 1u << 16;
     while (want < bytes) want *= 2;
-    if (dev) (void)hipFree(dev);
-    if (host) (void)hipHostFree(host);
-    dev = nullptr;
-    host = nullptr;
-    cap = 0;
-    if (hipMalloc(&dev, want) != hipSuccess) return KDB_LZ4_EHIP;
-    if (hipHostMalloc(&host, want, hipHostMallocDefault) != hipSuccess) return KDB_LZ4_EHIP;
-    cap = want;
+    return want;
+  }
+  int reserve(size_t host_bytes, size_t dev_bytes) {
+    if (!stream && hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return KDB_LZ4_EHIP;
+    if (host_bytes > hcap) {
+      if (host) (void)hipHostFree(host);
+      host = hdev = nullptr;
+      hcap = 0;
+      const size_t want = grow(0, host_bytes);
+      if (hipHostMalloc(&host, want, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return KDB_LZ4_EHIP;
+      if (hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), host, 0) != hipSuccess) return KDB_LZ4_EHIP;
+      hcap = want;
+    }
+    if (dev_bytes > dcap) {
+      if (dev) (void)hipFree(dev);
+      dev = nullptr;
+      dcap = 0;
+      const size_t want = grow(0, dev_bytes);
+      if (hipMalloc(&dev, want) != hipSuccess) return KDB_LZ4_EHIP;
+      dcap = want;
+    }
     return KDB_LZ4_OK;
   }
 };
@@ -78,8 +99,8 @@ ScalarCtx& scalar_ctx(int* err) {
   return ctxs[dev];
 }
 
-// Layout of the scalar staging buffer: a 64-byte metadata block (offsets,
-// lengths, caps, results) followed by input and output regions.
+// Layout of the scalar staging buffers: a 64-byte metadata block (offsets,
+// lengths, caps, results) followed by the input and output regions.
 struct Meta {
   uint64_t src_off, dst_off;
   uint32_t len, cap, target, out_len;
@@ -87,8 +108,18 @@ struct Meta {
 };
 static_assert(sizeof(Meta) <= 64, "meta block");
 constexpr size_t kMetaBytes = 64;
+// Largest value (compress) / output (decode) the zero-copy route takes: the
+// LDS-staged class kernels (lz4_compress.hip kMidLdsMax, the decoder's
+// default LDS split).
+constexpr uint32_t kZeroCopyMax = 8192u;
 
 inline size_t align16(size_t x) { return (x + 15u) & ~(size_t)15u; }
+
+inline Meta read_meta(const uint8_t* p) {
+  Meta m;
+  memcpy(&m, const_cast<const uint8_t*>(p), sizeof(m));
+  return m;
+}
 
 }  // namespace
 
@@ -153,35 +184,48 @@ int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize
   int err = 0;
   ScalarCtx& c = scalar_ctx(&err);
   if (err) return 0;
-  const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)inputSize + 16);
+  const uint32_t S = (uint32_t)inputSize;
   // The kernel never writes past the cap, and the cap never needs to exceed
   // the bound for the return value to be exact.
-  const uint32_t bound = compress_bound((uint32_t)inputSize);
+  const uint32_t bound = compress_bound(S);
   const uint32_t cap = (uint32_t)maxOutputSize < bound ? (uint32_t)maxOutputSize : bound;
-  if (c.reserve(out_at + align16(cap + 16)) != KDB_LZ4_OK) return 0;
   Meta m{};
-  m.src_off = in_at;
-  m.dst_off = out_at;
-  m.len = (uint32_t)inputSize;
+  m.len = S;
   m.cap = (uint32_t)maxOutputSize;
-  memcpy(c.host, &m, sizeof(m));
-  if (inputSize) memcpy(c.host + in_at, source, (size_t)inputSize);
-  Meta* dm = reinterpret_cast<Meta*>(c.dev);
-  if (hipMemcpyAsync(c.dev, c.host, in_at + (size_t)inputSize, hipMemcpyHostToDevice, c.stream) != hipSuccess)
-    return 0;
-  if (launch_compress(false, c.stream, c.dev, &dm->src_off, &dm->len, 1, (uint32_t)inputSize, c.dev,
-                      &dm->dst_off, &dm->cap, nullptr, &dm->ret) != hipSuccess)
-    return 0;
-  if (hipMemcpyAsync(c.host, c.dev, kMetaBytes, hipMemcpyDeviceToHost, c.stream) != hipSuccess) return 0;
-  if (hipStreamSynchronize(c.stream) != hipSuccess) return 0;
-  memcpy(&m, c.host, sizeof(m));
-  if (m.ret > 0) {
-    if (hipMemcpyAsync(c.host + out_at, c.dev + out_at, (size_t)m.ret, hipMemcpyDeviceToHost, c.stream) !=
-            hipSuccess ||
+  if (S <= kZeroCopyMax) {                       // zero-copy: [meta][in][out] in mapped host memory
+    const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)S + 16);
+    if (c.reserve(out_at + align16(cap + 16), 0) != KDB_LZ4_OK) return 0;
+    m.src_off = in_at;
+    m.dst_off = out_at;
+    memcpy(c.host, &m, sizeof(m));
+    if (S) memcpy(c.host + in_at, source, S);
+    Meta* dm = reinterpret_cast<Meta*>(c.hdev);
+    if (launch_compress(false, c.stream, c.hdev, &dm->src_off, &dm->len, 1, S, S, c.hdev, &dm->dst_off, &dm->cap,
+                        nullptr, &dm->ret) != hipSuccess ||
         hipStreamSynchronize(c.stream) != hipSuccess)
       return 0;
-    memcpy(dest, c.host + out_at, (size_t)m.ret);
+    m = read_meta(c.host);
+    if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
+    return m.ret > 0 ? m.ret : 0;
   }
+  // device staging: [meta][out][in]; one D2H of meta + the whole output slot
+  const size_t out_at = kMetaBytes, in_at = kMetaBytes + align16((size_t)cap + 16);
+  const size_t bytes = in_at + align16((size_t)S + 16);
+  if (c.reserve(bytes, bytes) != KDB_LZ4_OK) return 0;
+  m.src_off = in_at;
+  m.dst_off = out_at;
+  memcpy(c.host, &m, sizeof(m));
+  memcpy(c.host + in_at, source, S);
+  Meta* dm = reinterpret_cast<Meta*>(c.dev);
+  if (hipMemcpyAsync(c.dev, c.host, kMetaBytes, hipMemcpyHostToDevice, c.stream) != hipSuccess ||
+      hipMemcpyAsync(c.dev + in_at, c.host + in_at, S, hipMemcpyHostToDevice, c.stream) != hipSuccess ||
+      launch_compress(false, c.stream, c.dev, &dm->src_off, &dm->len, 1, S, S, c.dev, &dm->dst_off, &dm->cap,
+                      nullptr, &dm->ret) != hipSuccess ||
+      hipMemcpyAsync(c.host, c.dev, in_at, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+      hipStreamSynchronize(c.stream) != hipSuccess)
+    return 0;
+  m = read_meta(c.host);
+  if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
   return m.ret > 0 ? m.ret : 0;
 }
 
@@ -191,35 +235,49 @@ int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compress
   int err = 0;
   ScalarCtx& c = scalar_ctx(&err);
   if (err) return -1;
-  const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)compressedSize + 16);
-  if (c.reserve(out_at + align16((size_t)maxDecompressedSize + 16)) != KDB_LZ4_OK) return -1;
+  const uint32_t C = (uint32_t)compressedSize, O = (uint32_t)maxDecompressedSize;
   Meta m{};
-  m.src_off = in_at;
-  m.dst_off = out_at;
-  m.len = (uint32_t)compressedSize;
-  m.cap = (uint32_t)maxDecompressedSize;
+  m.len = C;
+  m.cap = O;
   m.target = (uint32_t)targetOutputSize;
-  memcpy(c.host, &m, sizeof(m));
-  if (compressedSize) memcpy(c.host + in_at, source, (size_t)compressedSize);
-  Meta* dm = reinterpret_cast<Meta*>(c.dev);
-  if (hipMemcpyAsync(c.dev, c.host, in_at + (size_t)compressedSize, hipMemcpyHostToDevice, c.stream) !=
-      hipSuccess)
-    return -1;
-  if (launch_decompress(false, c.stream, c.dev, &dm->src_off, &dm->len, 1, (uint32_t)compressedSize,
-                        (uint32_t)maxDecompressedSize, c.dev, &dm->dst_off, &dm->cap, &dm->target,
-                        &dm->out_len, &dm->ret) != hipSuccess)
-    return -1;
-  if (hipMemcpyAsync(c.host, c.dev, kMetaBytes, hipMemcpyDeviceToHost, c.stream) != hipSuccess) return -1;
-  if (hipStreamSynchronize(c.stream) != hipSuccess) return -1;
-  memcpy(&m, c.host, sizeof(m));
-  if (m.ret == KDB_LZ4_VALUE_UNSUPPORTED) return -1;
-  if (m.ret > 0) {
-    if (hipMemcpyAsync(c.host + out_at, c.dev + out_at, (size_t)m.ret, hipMemcpyDeviceToHost, c.stream) !=
-            hipSuccess ||
+  // the LDS-resident decoder's share (lz4_decompress.hip: output <= its split,
+  // block <= that output's bound + a frame header)
+  const bool zc = O <= kZeroCopyMax && C <= kZeroCopyMax + kZeroCopyMax / 255u + 24u;
+  if (zc) {                                      // zero-copy: [meta][in][out] in mapped host memory
+    const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)C + 16);
+    if (c.reserve(out_at + align16((size_t)O + 16), 0) != KDB_LZ4_OK) return -1;
+    m.src_off = in_at;
+    m.dst_off = out_at;
+    memcpy(c.host, &m, sizeof(m));
+    if (C) memcpy(c.host + in_at, source, C);
+    Meta* dm = reinterpret_cast<Meta*>(c.hdev);
+    if (launch_decompress(false, c.stream, c.hdev, &dm->src_off, &dm->len, 1, C, O, c.hdev, &dm->dst_off, &dm->cap,
+                          &dm->target, &dm->out_len, &dm->ret) != hipSuccess ||
         hipStreamSynchronize(c.stream) != hipSuccess)
       return -1;
-    memcpy(dest, c.host + out_at, (size_t)m.ret);
+    m = read_meta(c.host);
+    if (m.ret == KDB_LZ4_VALUE_UNSUPPORTED) return -1;
+    if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
+    return m.ret;
   }
+  const size_t out_at = kMetaBytes, in_at = kMetaBytes + align16((size_t)O + 16);
+  const size_t bytes = in_at + align16((size_t)C + 16);
+  if (c.reserve(bytes, bytes) != KDB_LZ4_OK) return -1;
+  m.src_off = in_at;
+  m.dst_off = out_at;
+  memcpy(c.host, &m, sizeof(m));
+  memcpy(c.host + in_at, source, C);
+  Meta* dm = reinterpret_cast<Meta*>(c.dev);
+  if (hipMemcpyAsync(c.dev, c.host, kMetaBytes, hipMemcpyHostToDevice, c.stream) != hipSuccess ||
+      hipMemcpyAsync(c.dev + in_at, c.host + in_at, C, hipMemcpyHostToDevice, c.stream) != hipSuccess ||
+      launch_decompress(false, c.stream, c.dev, &dm->src_off, &dm->len, 1, C, O, c.dev, &dm->dst_off, &dm->cap,
+                        &dm->target, &dm->out_len, &dm->ret) != hipSuccess ||
+      hipMemcpyAsync(c.host, c.dev, in_at, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
+      hipStreamSynchronize(c.stream) != hipSuccess)
+    return -1;
+  m = read_meta(c.host);
+  if (m.ret == KDB_LZ4_VALUE_UNSUPPORTED) return -1;
+  if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
   return m.ret;
 }
 
@@ -231,7 +289,7 @@ int kdb_lz4_compress_blocks_batch(void* stream, const uint8_t* src, const uint64
                                   const uint64_t* dst_off, const uint32_t* dst_cap, int32_t* ret) {
   if (n == 0) return KDB_LZ4_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !dst_cap || !ret) return KDB_LZ4_EINVAL;
-  return hip_status(launch_compress(false, (hipStream_t)stream, src, src_off, src_len, n, max_len, dst,
+  return hip_status(launch_compress(false, (hipStream_t)stream, src, src_off, src_len, n, 0u, max_len, dst,
                                     dst_off, dst_cap, nullptr, ret));
 }
 
@@ -250,7 +308,7 @@ int kdb_lz4_compress_frames_batch(void* stream, const uint8_t* src, const uint64
                                   const uint64_t* dst_off, uint32_t* frame_len, int32_t* status) {
   if (n == 0) return KDB_LZ4_OK;
   if (!src || !src_off || !src_len || !dst || !dst_off || !frame_len || !status) return KDB_LZ4_EINVAL;
-  return hip_status(launch_compress(true, (hipStream_t)stream, src, src_off, src_len, n, max_len, dst,
+  return hip_status(launch_compress(true, (hipStream_t)stream, src, src_off, src_len, n, 0u, max_len, dst,
                                     dst_off, nullptr, frame_len, status));
 }
 

@@ -5,6 +5,12 @@
 // util/status.h (Status, status.h:20-85) and util/byte_array.h (ByteArray,
 // byte_array.h:182-298).  These mirrors keep the same names, codes and the
 // members CompressorLZ4 touches, so the drop-in compiles identically in both.
+//
+// The mirrors live in the inline namespace kdb::standalone (and so does the
+// standalone CompressorLZ4, compressor.h): source still says kdb::Status,
+// but the mangled names differ from KingDB's, so an object built against the
+// mirrors can never be linked into a KingDB build by mistake -- the link
+// fails instead of two ByteArray layouts meeting at run time.
 #pragma once
 
 #ifdef KDB_LZ4_IN_KINGDB
@@ -18,6 +24,7 @@
 #include <string>
 
 namespace kdb {
+inline namespace standalone {
 
 // util/status.h:20-85 (codes status.h:72-79).
 class Status {
@@ -116,5 +123,6 @@ inline ByteArray NewShallowCopyByteArray(char* data, uint64_t size) {
   return ByteArray::NewShallowCopyByteArray(data, size);
 }
 
+}  // namespace standalone
 }  // namespace kdb
 #endif  // KDB_LZ4_IN_KINGDB

@@ -50,6 +50,12 @@ hipError_t work_counter(hipStream_t st, uint32_t** ctr) {
   return e;
 }
 
+hipError_t launch_counter(hipStream_t st, uint32_t n, uint32_t grid, uint32_t** ctr) {
+  *ctr = nullptr;
+  if (grid >= n) return hipSuccess;
+  return work_counter(st, ctr);
+}
+
 // Workgroups of 64 threads resident at once for `kern` with `lds` bytes of
 // dynamic LDS, capped at n (the kernels dequeue values dynamically, so a
 // workgroup that is admitted late simply takes fewer values).

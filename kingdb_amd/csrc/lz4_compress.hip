@@ -679,11 +679,18 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     grp.b = bins_s;
     for (uint32_t i = lane; i < BinGroup::kBytes / 8u; i += 64u) bins_s[i] = 0ull;
   }
+  bool direct_done = false;
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
-    if (lane == 0) c0 = atomicAdd(work, batch);
-    c0 = uni(c0);
+    if (!work) {                                 // direct launch: value blockIdx.x, once
+      if (direct_done) break;
+      c0 = blockIdx.x;
+      direct_done = true;
+    } else {
+      if (lane == 0) c0 = atomicAdd(work, batch);
+      c0 = uni(c0);
+    }
     if (c0 >= n) break;
     const uint32_t vi = c0 + lane;
     const bool in_claim = lane < batch && vi < n;
@@ -759,10 +766,10 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0) {
   auto kern = lz4_compress_kernel<F, Sm, Bn>;
-  uint32_t* work = nullptr;
-  hipError_t e = work_counter(st, &work);
-  if (e != hipSuccess) return e;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  uint32_t* work = nullptr;
+  hipError_t e = launch_counter(st, n, grid, &work);
+  if (e != hipSuccess) return e;
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap));
@@ -781,67 +788,74 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   }();
   auto kern = bins ? lz4_compress_big_kernel<F, W, true> : lz4_compress_big_kernel<F, W, false>;
   static const uint32_t prio = env_prio();
-  uint32_t* work = nullptr;
-  hipError_t e = work_counter(st, &work);
-  if (e != hipSuccess) return e;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
-  const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
+  uint32_t* work = nullptr;
+  hipError_t e = launch_counter(st, n, grid, &work);
+  if (e != hipSuccess) return e;
+  const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, prio);
   return hipGetLastError();
 }
 
-// One launch per size class present up to max_len: <= 4 KiB (tagged table,
-// 20 KiB LDS: 8 values per CU), 4 KiB .. 65 546 B (LDS sized for the largest),
-// >= 65 547 B (byU32, in place).  Each launch skips the other classes' values.
+// One launch per size class that [min_len, max_len] (the launch's bounds on
+// its values' lengths; the batch API passes min_len 0) intersects: <= 4 KiB
+// (two-plane table, 16 KiB LDS), 4 KiB .. 8 KiB (LDS-staged), 8 KiB .. 65 546 B
+// (in place, byU16), >= 65 547 B (byU32, in place).  Each launch skips the
+// other classes' values; with several classes a census kernel lets a class
+// launch with nothing to do return at once.
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
-                           const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
+                           const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret) {
   if (n == 0) return hipSuccess;
+  if (min_len > max_len) min_len = 0;
   hipError_t e;
-  static const uint32_t mid_split_env = [] {
+  static const uint32_t mid_split = [] {
     const char* v = getenv("KDB_LZ4_CSPLIT");
     return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : kMidLdsMax;
   }();
-  uint32_t* census = nullptr;            // per-class counts, when more than one class may launch
-  if (max_len > kSmallMax) {
+  const uint32_t b1 = min(max(mid_split, kSmallMax), k64KLimit - 1u);   // top of the LDS-staged class
+  // class c covers lengths [lo[c], hi[c]]
+  const uint32_t lo[4] = {0u, kSmallMax + 1u, b1 + 1u, k64KLimit};
+  const uint32_t hi[4] = {kSmallMax, b1, k64KLimit - 1u, 0xFFFFFFFFu};
+  bool on[4];
+  uint32_t classes = 0;
+  for (int c = 0; c < 4; ++c) {
+    on[c] = lo[c] <= hi[c] && max_len >= lo[c] && min_len <= hi[c];
+    classes += on[c] ? 1u : 0u;
+  }
+  uint32_t* census = nullptr;            // per-class counts, when more than one class launches
+  if (classes > 1) {
     e = work_counter(st, &census);
     if (e != hipSuccess) return e;
-    const uint32_t b1 = min(max(mid_split_env, kSmallMax), k64KLimit - 1u);
     hipLaunchKernelGGL(class_census_kernel, dim3(min((n + 255u) / 256u, 1024u)), dim3(256), 0, st, src_len, n,
                        kSmallMax, b1, k64KLimit - 1u, census);
   }
   // The in-place classes (8 KiB .. 65 546 B, and byU32) go first, on a
-  // forked stream: their values take longest, and the small classes fill the
-  // GPU around their tail.
-  static const uint32_t mid_split = [] {
-    const char* e = getenv("KDB_LZ4_CSPLIT");
-    return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : kMidLdsMax;
-  }();
-  const uint32_t glo = max(mid_split, kSmallMax) + 1u;
-  const bool in_place = max_len >= glo;
+  // forked stream when smaller classes follow: their values take longest,
+  // and the small classes fill the GPU around their tail.
   hipStream_t aux = st;
-  if (in_place) {
+  const bool fork = (on[2] || on[3]) && (on[0] || on[1]);
+  if (fork) {
     e = fork_begin(st, &aux);
     if (e != hipSuccess) return e;
   }
-  if (max_len >= glo && glo < k64KLimit) {
-    const uint32_t cap = max_len < k64KLimit ? max_len : k64KLimit - 1u;
-    e = frame ? launch_big<true, false>(aux, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
+  if (on[2]) {
+    e = frame ? launch_big<true, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
                                         ret, census, 2)
-              : launch_big<false, false>(aux, src, src_off, src_len, n, glo, cap, dst, dst_off, dst_cap, frame_len,
+              : launch_big<false, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
                                          ret, census, 2);
     if (e != hipSuccess) return e;
   }
-  if (max_len >= k64KLimit) {
-    e = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
+  if (on[3]) {
+    e = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
                                        frame_len, ret, census, 3)
-              : launch_big<false, true>(aux, src, src_off, src_len, n, k64KLimit, 0xFFFFFFFFu, dst, dst_off, dst_cap,
+              : launch_big<false, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
                                         frame_len, ret, census, 3);
     if (e != hipSuccess) return e;
   }
-  {
+  if (on[0]) {
     // KDB_LZ4_GROUP=ballot: the 13-ballot grouping at 10 per CU (A/B diagnostic)
     static const bool bins = [] {
       const char* g = getenv("KDB_LZ4_GROUP");
@@ -863,16 +877,16 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
   // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
   // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
-  if (max_len > kSmallMax && mid_split > kSmallMax) {
-    const uint32_t hi = min(min(max_len, mid_split), k64KLimit - 1u);
-    const size_t lds = compress_lds_bytes(hi, false);
-    e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
+  if (on[1]) {
+    const uint32_t top = min(max_len, hi[1]);
+    const size_t lds = compress_lds_bytes(top, false);
+    e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
                                         dst_cap, frame_len, ret, census, 1)
-              : launch_one<false, false>(st, lds, src, src_off, src_len, n, kSmallMax + 1u, hi, dst, dst_off,
+              : launch_one<false, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
                                          dst_cap, frame_len, ret, census, 1);
     if (e != hipSuccess) return e;
   }
-  return fork_end(st, aux);
+  return fork ? fork_end(st, aux) : hipSuccess;
 }
 
 }  // namespace kdb_lz4

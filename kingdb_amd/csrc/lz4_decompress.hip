@@ -595,11 +595,18 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
   const uint32_t lane = lane_id();
   uint8_t* ring = smem;
   uint8_t* iring = smem + kORing;
+  bool direct_done = false;
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
-    if (lane == 0) c0 = atomicAdd(work, batch);
-    c0 = uni(c0);
+    if (!work) {                                 // direct launch: value blockIdx.x, once
+      if (direct_done) break;
+      c0 = blockIdx.x;
+      direct_done = true;
+    } else {
+      if (lane == 0) c0 = atomicAdd(work, batch);
+      c0 = uni(c0);
+    }
     if (c0 >= n) break;
     const uint32_t vi = c0 + lane;
     bool mine = false;
@@ -690,10 +697,10 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
                              const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
                              uint32_t* out_len, int32_t* ret, uint32_t skip_big) {
   auto kern = lz4_decompress_kernel<F>;
-  uint32_t* work = nullptr;
-  hipError_t e = work_counter(st, &work);
-  if (e != hipSuccess) return e;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  uint32_t* work = nullptr;
+  hipError_t e = launch_counter(st, n, grid, &work);
+  if (e != hipSuccess) return e;
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
                      out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out));
@@ -706,12 +713,12 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                              const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   auto kern = lz4_decompress_big_kernel<F, R>;
   static const uint32_t prio = env_prio();
-  uint32_t* work = nullptr;
-  hipError_t e = work_counter(st, &work);
-  if (e != hipSuccess) return e;
   const size_t lds = ring_lds<R>();
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
-  const uint32_t batch = claim_batch(n, grid);   // values per claim; lanes >= batch idle
+  uint32_t* work = nullptr;
+  hipError_t e = launch_counter(st, n, grid, &work);
+  if (e != hipSuccess) return e;
+  const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
                      dst_off, out_cap, target, out_len, ret, work, batch, prio);
   return hipGetLastError();
@@ -766,11 +773,14 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
   // longest); the two launches write disjoint values
   hipStream_t aux = st;
   hipError_t e = hipSuccess;
+  // one block that the ring decoder owns (a scalar call): that launch alone
+  const bool ring_only = !frame && n == 1u && big;
   if (big) {
-    if ((e = fork_begin(st, &aux)) != hipSuccess) return e;
+    if (!ring_only && (e = fork_begin(st, &aux)) != hipSuccess) return e;
     e = frame ? launch_ring<true>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
               : launch_ring<false>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
     if (e != hipSuccess) return e;
+    if (ring_only) return hipSuccess;
   }
   e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
                                out_len, ret, big ? 1u : 0u)

@@ -66,7 +66,10 @@ struct WorkQueue {
   uint32_t n, batch, cur, end, nr, q, left;
   // nr ranges: 1, or kQueues for launches whose claim rate would saturate one
   // counter (work_queues() on the host picks)
+  // c == nullptr: a direct launch (grid == n, see direct_grid), workgroup b
+  // takes value b and nothing else -- no counter, so no memset before it.
   __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr) {
+    if (!c) return WorkQueue{c, n, batch, blockIdx.x, min(blockIdx.x + 1u, n), 1u, 0u, 0u};
     nr = nr > 1u ? kQueues : 1u;
     return WorkQueue{c, n, batch, 0u, 0u, nr, (uint32_t)blockIdx.x % nr, nr};
   }
@@ -154,6 +157,10 @@ __device__ __forceinline__ void flush_lds_to_global(uint8_t* g, const uint8_t* l
 
 hipError_t work_counter(hipStream_t st, uint32_t** ctr);
 uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
+// The launch's work counter: a direct launch (n no larger than the resident
+// grid, so one value per workgroup) needs none (*ctr = nullptr, no memset:
+// the scalar entry points' latency); otherwise a zeroed counter slot.
+hipError_t launch_counter(hipStream_t st, uint32_t n, uint32_t grid, uint32_t** ctr);
 uint32_t claim_batch(uint32_t n, uint32_t grid);
 // WorkQueue ranges for a launch whose values are at most max_len bytes
 uint32_t work_queues(uint32_t max_len);

@@ -47,7 +47,7 @@
 namespace kdb_lz4 {
 
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
-                           const uint32_t* src_len, uint32_t n, uint32_t max_len, uint8_t* dst,
+                           const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret);
 hipError_t launch_exclusive_scan(hipStream_t st, const uint32_t* len, uint32_t n, uint64_t* off, uint64_t* total);
@@ -584,7 +584,7 @@ hipError_t launch_put_entries(hipStream_t st, const uint8_t* keys, const uint64_
   if (nparts) {
     hipError_t e = launch_exclusive_scan(st, part_slot, nparts, frame_off, ftotal);
     if (e != hipSuccess) return e;
-    e = launch_compress(true, st, values, part_src, chunk_len, nparts, max_chunk, frames, frame_off,
+    e = launch_compress(true, st, values, part_src, chunk_len, nparts, 0u, max_chunk, frames, frame_off,
                                    nullptr, frame_len, fstatus);
     if (e != hipSuccess) return e;
   }

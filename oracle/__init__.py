@@ -111,6 +111,16 @@ class Oracle:
         a = np.frombuffer(data, dtype=np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
         return self.lib.orc_crc32c_extend(crc, _ptr(a), len(data))
 
+    def crc32c_array(self, a: np.ndarray, crc: int = 0) -> int:
+        """CRC32C of a contiguous uint8 array, no copy (GB-sized streams)."""
+        a = np.ascontiguousarray(a, dtype=np.uint8)
+        return self.lib.orc_crc32c_extend(crc, _ptr(a), a.nbytes) if a.nbytes else crc
+
+    def frames_digest(self, src: np.ndarray, off: np.ndarray, lens: np.ndarray) -> tuple[int, int]:
+        """(sum of frame bytes, CRC32C of the frames concatenated) of CompressorLZ4
+        frames of values src[off[i] .. +lens[i]) (tests/golden/digests.json)."""
+        return _digest(self.lib.orc_frames_digest, src, off, lens)
+
     def g1_pieces(self, npieces: int, seed: int = 301) -> np.ndarray:
         out = np.empty(npieces * 100, dtype=np.uint8)
         self.lib.orc_g1_pieces(seed, npieces, _ptr(out))
@@ -169,6 +179,22 @@ class Oracle:
         parts = [(int(po[i]), stored[int(po[i]):int(po[i]) + int(pl[i])].tobytes()) for i in range(n)]
         return {"parts": parts, "svc": svc.value, "crc": crc.value,
                 "stored": stored[: len(value) + self.padding(len(value))].tobytes()}
+
+
+def _digest(fn, src: np.ndarray, off: np.ndarray, lens: np.ndarray) -> tuple[int, int]:
+    c = ctypes
+    fn.argtypes = [_u8p, c.POINTER(c.c_uint64), c.POINTER(c.c_uint32), c.c_uint64, c.POINTER(c.c_uint64),
+                   c.POINTER(c.c_uint32)]
+    fn.restype = c.c_int
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.uint32)
+    tot, crc = c.c_uint64(0), c.c_uint32(0)
+    r = fn(_ptr(src), off.ctypes.data_as(c.POINTER(c.c_uint64)), lens.ctypes.data_as(c.POINTER(c.c_uint32)),
+           len(lens), c.byref(tot), c.byref(crc))
+    if r != 0:
+        raise RuntimeError("frames_digest: IOError")
+    return tot.value, crc.value
 
 
 class Reference:
@@ -232,6 +258,11 @@ class Reference:
     def crc32c(self, data: bytes, crc: int = 0) -> int:
         a = np.frombuffer(data, dtype=np.uint8).copy() if len(data) else np.zeros(1, np.uint8)
         return self.lib.ref_crc32c_extend(crc, _ptr(a), len(data))
+
+    def frames_digest(self, src: np.ndarray, off: np.ndarray, lens: np.ndarray) -> tuple[int, int]:
+        """The reference's CompressorLZ4::Compress over every value: (sum of frame
+        bytes, CRC32C of the frames concatenated)."""
+        return _digest(self.lib.ref_frames_digest, src, off, lens)
 
     def uncompress_value(self, stored: bytes, svc: int, size: int, checksum: int = 0, checksum_initial: int = 0,
                          verify: bool = False) -> tuple[int, bytes]:

@@ -317,6 +317,36 @@ int64_t orc_frame_compress(const uint8_t* src, uint64_t n, uint8_t* frame) {
 }
 
 /*
+ * Digest of a batch of frames (values src[off[i] .. +len[i]) in order):
+ * *total = sum of frame lengths, *crc = CRC32C of the frames concatenated.
+ * The same digest oracle/ref_shim.cc's ref_frames_digest takes of the
+ * reference's frames (tests/golden/digests.json).  -1 on IOError.
+ */
+int orc_frames_digest(const uint8_t* src, const uint64_t* off, const uint32_t* len, uint64_t n,
+                      uint64_t* total, uint32_t* crc) {
+  uint64_t t = 0, cap = 0;
+  uint32_t x = 0;
+  uint8_t* fr = NULL;
+  for (uint64_t i = 0; i < n; i++) {
+    uint64_t need = 8 + (uint64_t)orc_compress_bound((int)len[i]) + len[i] + 64;
+    if (need > cap) {
+      free(fr);
+      cap = need;
+      fr = (uint8_t*)malloc(cap);
+      if (!fr) return -1;
+    }
+    int64_t f = orc_frame_compress(src + off[i], len[i], fr);
+    if (f < 0) { free(fr); return -1; }
+    x = orc_crc32c_extend(x, fr, (size_t)f);
+    t += (uint64_t)f;
+  }
+  free(fr);
+  *total = t;
+  *crc = x;
+  return 0;
+}
+
+/*
  * CompressorLZ4::Uncompress of ONE frame at `frame` (compressor.cc:75-137),
  * do_memory_allocation=false flavour.  Returns 0 (OK) and sets *out_n and
  * *frame_n, or -1 (IOError) when the block decoder returns <= 0.

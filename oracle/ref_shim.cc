@@ -81,6 +81,30 @@ uint32_t ref_crc32c_extend(uint32_t crc, const char* p, uint64_t n) {
   return kdb::crc32c::Extend(crc, p, n);
 }
 
+// Digest of a whole batch of CompressorLZ4::Compress frames (values
+// src[off[i] .. +len[i]) in order): *total = sum of frame lengths, *crc =
+// crc32c::Extend over the frames concatenated.  Pins byte identity at the
+// BASELINE sizes (tests/golden/make_digests.py) without committing GBs.
+// Returns -1 on the first IOError, else 0.
+int ref_frames_digest(const char* src, const uint64_t* off, const uint32_t* len, uint64_t n, uint64_t* total,
+                      uint32_t* crc) {
+  kdb::CompressorLZ4 c;
+  uint64_t t = 0;
+  uint32_t x = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    char* frame = nullptr;
+    uint64_t fn = 0;
+    kdb::Status s = c.Compress(const_cast<char*>(src) + off[i], len[i], &frame, &fn);
+    if (!s.IsOK()) return -1;
+    x = kdb::crc32c::Extend(x, frame, fn);
+    t += fn;
+    delete[] frame;
+  }
+  *total = t;
+  *crc = x;
+  return 0;
+}
+
 // G2: test_db.cc:108-131, one generator instance, `count` successive calls.
 void ref_gen_g2(char* out, int size, int count) {
   std::seed_seq seq{1, 2, 3, 4, 5, 6, 7};

@@ -2,10 +2,12 @@
 
 Pins the oracle: every expected byte here came from the reference's own
 algorithm/lz4.cc + compressor.cc (tests/golden/make_golden.py)."""
+import os
+
 import numpy as np
 
 import oracle
-from conftest import load_golden, split
+from conftest import GOLDEN, load_golden, split
 
 
 def test_kat_blocks_and_frames(orc):
@@ -115,3 +117,22 @@ def test_big_values_byu32(orc):
     for (kind, pos, val), ret in zip(g["mal_recipe"], g["mal_ret"]):
         r, _ = orc.decompress(apply_recipe(base, int(kind), int(pos), int(val)), 1 << 20)
         assert r == int(ret), (kind, pos, val)
+
+
+def test_oracle_matches_reference_digests_prefix(orc):
+    """tests/golden/digests.json (the reference's frames at BASELINE size,
+    make_digests.py): the oracle's frames of each batch's first 65 536 values
+    have the same byte count and CRC32C."""
+    import json
+    from kingdb_amd.lz4 import mixed_sizes
+    d = json.load(open(os.path.join(GOLDEN, "digests.json")))
+    for name, sizes in (("g1_long_4k", np.full(1 << 20, 4096, np.uint32)), ("mixed_1m", mixed_sizes(1 << 20))):
+        g = d[name]
+        assert g["n"] == len(sizes) and g["raw_bytes"] == int(sizes.astype(np.int64).sum())
+        k = g["prefix_n"]
+        lens = sizes[:k]
+        off = np.zeros(k, np.uint64)
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        src = orc.g1_pieces((int(lens.astype(np.int64).sum()) + 99) // 100)
+        tot, crc = orc.frames_digest(src, off, lens)
+        assert (tot, f"0x{crc:08x}") == (g["prefix_frame_bytes"], g["prefix_frames_crc32c"]), name

@@ -1,0 +1,92 @@
+#!/bin/bash
+# One parametrised GPU-box session (replaces the round-1 ad-hoc scripts).
+#
+#   gpurun --timeout 1200 -- bash tools/gpurun/run.sh <tag> <step> [<step> ...]
+#
+# Steps (run in the order given, each under its own time limit; the session
+# stops at the first failure and starts nothing more on the GPU):
+#   tests      pytest -m gpu
+#   smoke      __graft_entry__.smoke()
+#   bench      the headline line (bench.py, host-inclusive rate + CPU baseline)
+#   quick      the headline line without the CPU baseline / host-inclusive legs
+#   mixed put get   the other BASELINE workloads (bench.py --workload ...)
+#   prof       rocprofv3 --kernel-trace --stats of the headline bench
+#   profmixed profput profget   the same for the other workloads
+#   pmc        FETCH_SIZE / WRITE_SIZE passes of the headline -> pmc_traffic.json
+#   pmcmixed   the same for the mixed batch
+#   sq         SQ counter passes of the headline (tools/pmc.sh)
+#   dropin     KingDB's unit tests built against the drop-in (tests/test_kingdb_dropin.py)
+#   dropinfull the same with the whole test_db and client_emb (KDB_DROPIN_FULL=1)
+#   scalar     per-call latency of CompressorLZ4::Compress/Uncompress, drop-in vs reference
+#   ab:<NAME>=<VAL>  the quick headline line with one environment knob set
+# Outputs land in gpurun_out/<tag>_*.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+tag=$1; shift
+O=gpurun_out/$tag
+R=$GRAFT_REPO_ROOT
+say() { echo "== $tag $1 $(date +%T)"; }
+fail() { echo "$1 rc=$2"; tail -30 "$3"; exit 1; }
+line() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[1],d['metric'],d['value'],d.get('kernels_ms'),d.get('roofline',{}).get('frac'))" "$1"; }
+prof() {  # prof <name> <bench args...>
+  local n=$1; shift
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/${O}_prof_$n" -o "$n" -- python3 "$R/bench.py" "$@" > "${O}_prof_$n.json" 2> "${O}_prof_$n.err" || fail "prof $n" $? "${O}_prof_$n.err"
+  line "${O}_prof_$n.json"
+}
+pmc() {  # pmc <name> <n_values> <size> <bench args...>
+  local n=$1 nv=$2 sz=$3; shift 3
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/${O}_pmc_${n}_$c" -o pmc -- python3 "$R/bench.py" --no-cpu-baseline --no-verify --steps 1 --warmup 0 "$@" > "${O}_pmc_${n}_$c.log" 2>&1 || fail "pmc $n $c" $? "${O}_pmc_${n}_$c.log"
+  done
+  python tools/pmc_traffic.py "${O}_pmc_${n}_FETCH_SIZE" "${O}_pmc_${n}_WRITE_SIZE" "$nv" "$sz" "${O}_pmc_traffic_$n.json" || exit 1
+  cat "${O}_pmc_traffic_$n.json"
+}
+for s in "$@"; do
+  say "$s"
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "${O}_tests.log" 2>&1 || fail tests $? "${O}_tests.log"
+      tail -2 "${O}_tests.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "${O}_smoke.log" 2>&1 || fail smoke $? "${O}_smoke.log"
+      cat "${O}_smoke.log" ;;
+    bench)
+      timeout -k 10 600 python bench.py --host-inclusive > "${O}_bench.json" 2> "${O}_bench.err" || fail bench $? "${O}_bench.err"
+      cat "${O}_bench.json" ;;
+    quick)
+      timeout -k 10 300 python bench.py --no-cpu-baseline > "${O}_quick.json" 2> "${O}_quick.err" || fail quick $? "${O}_quick.err"
+      line "${O}_quick.json" ;;
+    mixed|put|get)
+      timeout -k 10 500 python bench.py --workload $s > "${O}_$s.json" 2> "${O}_$s.err" || fail $s $? "${O}_$s.err"
+      cat "${O}_$s.json" ;;
+    prof) prof bench --no-cpu-baseline --steps 5 --warmup 1 ;;
+    profmixed) prof mixed --workload mixed --no-cpu-baseline --steps 3 --warmup 1 ;;
+    profput) prof put --workload put --no-cpu-baseline --steps 3 --warmup 1 ;;
+    profget) prof get --workload get --no-cpu-baseline --steps 3 --warmup 1 ;;
+    pmc) pmc bench 1048576 4096 ;;
+    pmcmixed) pmc mixed 1048576 mixed --workload mixed ;;
+    sq)
+      timeout -k 10 900 bash tools/pmc.sh "${O}_sq" python3 "$R/bench.py" --no-cpu-baseline --no-verify --steps 1 --warmup 0 || exit 1
+      python tools/pmc_summary.py "${O}_sq" > "${O}_sq.txt" && cat "${O}_sq.txt" ;;
+    dropin|dropinfull)
+      [ $s = dropinfull ] && export KDB_DROPIN_FULL=1
+      timeout -k 10 1100 python -u -m pytest tests/test_kingdb_dropin.py -x -v -s -m gpu --durations=0 --timeout 1000 --timeout-method thread > "${O}_$s.log" 2>&1 || fail $s $? "${O}_$s.log"
+      grep -E "PASSED|FAILED|passed|failed|done in|count items|s call" "${O}_$s.log" | tail -30
+      unset KDB_DROPIN_FULL ;;
+    scalar)   # per-call latency of CompressorLZ4, drop-in (GPU) vs reference codec (CPU)
+      for sz in 100 4096 65536; do
+        for v in kingdb_ref kingdb_dropin; do
+          timeout -k 10 300 oracle/_ref/$v/bench_compressor $sz 2000 > "${O}_scalar_${v}_$sz.json" || fail "scalar $v $sz" $? "${O}_scalar_${v}_$sz.json"
+          echo "$v $(cat ${O}_scalar_${v}_$sz.json)"
+        done
+      done ;;
+    ab:*)
+      kv=${s#ab:}
+      env "$kv" timeout -k 10 300 python bench.py --no-cpu-baseline > "${O}_ab_${kv}.json" 2> "${O}_ab.err" || fail "ab $kv" $? "${O}_ab.err"
+      line "${O}_ab_${kv}.json" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+say done
