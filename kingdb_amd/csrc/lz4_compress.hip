@@ -52,6 +52,13 @@ __device__ __forceinline__ uint32_t search_pos(uint32_t s, uint32_t k) {
   return s + 1u + 32u * q * (q - 1u) + q * (r + 1u);
 }
 __device__ __forceinline__ uint32_t search_step(uint32_t k) { return k == 0 ? 1u : (63u + k) >> 6; }
+// p(k) for k >= 1 (chunks after the first: k >= 61), no k == 0 case to select
+template <bool kWide>
+__device__ __forceinline__ uint32_t search_pos_nz(uint32_t s, uint32_t k) {
+  const uint32_t nn = 62u + k, q = nn >> 6, r = nn & 63u;
+  if (kWide) return (uint32_t)min((uint64_t)s + 1u + 32ull * q * (q - 1u) + (uint64_t)q * (r + 1u), 0xFFFFFFFFull);
+  return s + 1u + 32u * q * (q - 1u) + q * (r + 1u);
+}
 
 __device__ __forceinline__ uint32_t hash16(uint32_t seq) { return (seq * 2654435761u) >> 19; }
 // lz4.cc:373-379: byU16 hashes to 13 bits, byU32 to 12
@@ -59,51 +66,93 @@ template <bool kWide>
 __device__ __forceinline__ uint32_t hashp(uint32_t seq) { return (seq * 2654435761u) >> (kWide ? 20 : 19); }
 
 
-// The byU16 table.  kTagged: entry = gen << 12 | pos (values <= 4 KiB, so
-// positions < 4096); an entry of another generation is an empty slot (0).
-template <bool kTagged>
-struct Table {
-  uint16_t* t;
-  uint32_t gen;
-  __device__ __forceinline__ uint32_t get(uint32_t h) const {
-    const uint32_t e = t[h];
-    if (kTagged) return (e >> 12) == gen ? (e & 0xfffu) : 0u;
-    return e;
-  }
-  __device__ __forceinline__ void put(uint32_t h, uint32_t p) const {
-    t[h] = (uint16_t)(kTagged ? ((gen << 12) | p) : p);
-  }
-};
+// ---------------------------------------------------------------- hash tables
+//
+// A search chunk evaluates 64 iterations of the search loop at once, and
+// iteration k's get must see every put of iterations < k (lz4.cc:505-523: get
+// then put, per iteration).  gfx950's LDS resolves the lanes of ONE
+// instruction that hit the same dword in ascending lane order -- a
+// read-modify-write with return gives lane i the word as lanes < i left it
+// (measured: tools/probe/lds_order.hip, 0 exceptions in 128 000 lanes).  So a
+// single ds_mskor_rtn_b32 per table plane is the whole get+put of a chunk:
+// lane i reads the entry of its slot as the nearest lower lane of the same
+// slot wrote it -- or as the chunk found it -- and writes its own position.
+// That is the sequential table, up to the lane that matches; the puts of the
+// lanes after it (which the sequential loop never makes) are undone by
+// restore(), by the one lane per slot whose entry came from before them.
+//
+// mskor: D = (D & ~mask) | data, on the dword holding the slot's field; a
+// lane with on = false passes mask 0 AND data 0 (no change) and still reads.
+
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+
+// Two masked-or exchanges with return, one wait: the compiler does not count
+// lgkmcnt for inline asm, so the asm waits for its own results.
+__device__ __forceinline__ void mskor_rtn2(uint32_t a0, uint32_t m0, uint32_t d0, uint32_t& r0, uint32_t a1,
+                                           uint32_t m1, uint32_t d1, uint32_t& r1) {
+  asm volatile(
+      "ds_mskor_rtn_b32 %0, %2, %3, %4\n\t"
+      "ds_mskor_rtn_b32 %1, %5, %6, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r0), "=&v"(r1)
+      : "v"(a0), "v"(m0), "v"(d0), "v"(a1), "v"(m1), "v"(d1)
+      : "memory");
+}
+__device__ __forceinline__ uint32_t mskor_rtn(uint32_t a, uint32_t m, uint32_t d) {
+  uint32_t r;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r) : "v"(a), "v"(m), "v"(d)
+               : "memory");
+  return r;
+}
+__device__ __forceinline__ void mskor(uint32_t a, uint32_t m, uint32_t d) {
+  asm volatile("ds_mskor_b32 %0, %1, %2" ::"v"(a), "v"(m), "v"(d) : "memory");
+}
 
 // byU16 table for values <= 4 KiB, whose positions fit 12 bits: two planes,
 // the low bytes (8192 x u8) and the high nibbles (4096 x u8, two per byte),
 // 12 KiB instead of 16 -- 16 KiB of LDS per value with its bytes, so 10
-// values per CU instead of 8 (the parse is latency-bound: occupancy is speed).
-// Cleared per value (12 x 16 B stores per lane).  The nibble half is written
-// with LDS and/or atomics: two lanes of one chunk may own the two nibbles of
-// one byte (hashes 2k, 2k+1).
+// values per CU (the parse is latency-bound: occupancy is speed).  Cleared per
+// value (12 x 16 B stores per lane).
 struct Table12 {
   uint8_t* lo;
   uint8_t* hi;
-  __device__ __forceinline__ uint32_t get(uint32_t h) const {
-    const uint32_t a = lo[h], b = hi[h >> 1];
-    return a | (((b >> ((h & 1u) << 2)) & 15u) << 8);
+  // get-then-put of every lane of the chunk, in lane order (see above)
+  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
+    const uint32_t sl = (h & 3u) << 3, sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
+    const uint32_t ml = on ? 0xffu << sl : 0u, mh = on ? 15u << sh : 0u;
+    uint32_t ol, oh;
+    mskor_rtn2(lds_off(lo) + (h & ~3u), ml, ((p & 0xffu) << sl) & ml, ol, lds_off(hi) + ((h >> 1) & ~3u), mh,
+               (((p >> 8) & 15u) << sh) & mh, oh);
+    return ((ol >> sl) & 0xffu) | (((oh >> sh) & 15u) << 8);
   }
-  __device__ __forceinline__ void put(uint32_t h, uint32_t p) const {
-    lo[h] = (uint8_t)p;
-    uint32_t* w = reinterpret_cast<uint32_t*>(hi + ((h >> 1) & ~3u));
+  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const {
+    lo[h] = (uint8_t)v;
     const uint32_t sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
-    __hip_atomic_fetch_and(w, ~(15u << sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_or(w, ((p >> 8) & 15u) << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    mskor(lds_off(hi) + ((h >> 1) & ~3u), 15u << sh, ((v >> 8) & 15u) << sh);
   }
 };
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
 
+// byU16 table, 8192 x u16 (values up to 65 546 bytes; positions < 65 536).
+struct Table16 {
+  uint16_t* t;
+  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
+    const uint32_t sh = (h & 1u) << 4, m = on ? 0xffffu << sh : 0u;
+    const uint32_t o = mskor_rtn(lds_off(t) + ((h & ~1u) << 1), m, ((p & 0xffffu) << sh) & m);
+    return (o >> sh) & 0xffffu;
+  }
+  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { t[h] = (uint16_t)v; }
+};
+
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
 struct Table32 {
   uint32_t* t;
-  __device__ __forceinline__ uint32_t get(uint32_t h) const { return t[h]; }
-  __device__ __forceinline__ void put(uint32_t h, uint32_t p) const { t[h] = p; }
+  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
+    return mskor_rtn(lds_off(t) + (h << 2), on ? 0xffffffffu : 0u, on ? p : 0u);
+  }
+  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { t[h] = v; }
 };
 
 // Value bytes staged in LDS (byte i at p[i]).
@@ -202,71 +251,12 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
-// Same-slot grouping of a search chunk: for each lane, the valid lanes of the
-// chunk whose positions hash to its table slot (itself included).
-//
-// BallotGroup: bit-sliced match-any, one ballot per hash bit.
-template <int kHashBits>
-struct BallotGroup {
-  __device__ __forceinline__ uint64_t same(uint32_t h, bool, uint64_t vm) const {
-    uint32_t lo = ~0u, hi = ~0u;
-#pragma unroll
-    for (int bb = 0; bb < kHashBits; bb += 2) {
-      // t = 0 or ~0 (one v_bfe_i32); the empty asm keeps the ballot on t
-      // itself instead of a second shift + compare of h.  Bits go in pairs
-      // so each ballot's SGPR write is not read by the very next VALU op
-      // (no s_nop wait states).
-      uint32_t t0 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb, 1);
-      uint32_t t1 = (uint32_t)__builtin_amdgcn_sbfe((int)h, bb + 1 < kHashBits ? bb + 1 : bb, 1);
-      asm volatile("" : "+v"(t0), "+v"(t1));
-      const uint64_t m0 = ballot(t0 != 0u);
-      const uint64_t m1 = ballot(t1 != 0u);
-      // acc & ~(t ^ m) in one v_bitop3 per half (truth table 0x90)
-      lo = __builtin_amdgcn_bitop3_b32(lo, t0, (uint32_t)m0, 0x90);
-      hi = __builtin_amdgcn_bitop3_b32(hi, t0, (uint32_t)(m0 >> 32), 0x90);
-      if (bb + 1 < kHashBits) {
-        lo = __builtin_amdgcn_bitop3_b32(lo, t1, (uint32_t)m1, 0x90);
-        hi = __builtin_amdgcn_bitop3_b32(hi, t1, (uint32_t)(m1 >> 32), 0x90);
-      }
-    }
-    return (((uint64_t)hi << 32) | lo) & vm;
-  }
-};
-
-// BinGroup: two LDS bins per slot, slot & 127 and slot >> 7, each holding a
-// 64-bit lane mask that the chunk's valid lanes OR themselves into
-// (ds_or_b64).  Lanes found in both of my bins agree on every hash bit, so the
-// intersection is exactly my group.  Two atomics, two reads and two clears
-// (LDS runs one wave's ops in order) and a few VALU, in place of 13 ballots
-// and ~45 VALU; 1.5 KiB of LDS per wave, all zero between chunks.
-struct BinGroup {
-  uint64_t* b;
-  static constexpr uint32_t kBytes = (128u + 64u) * 8u;
-  __device__ __forceinline__ uint64_t same(uint32_t h, bool, uint64_t vm) const {
-    uint64_t* b0 = b + (h & 127u);
-    uint64_t* b1 = b + 128u + (h >> 7);
-    asm volatile("" ::: "memory");
-    // every lane ORs (its bit if valid, else 0): no exec-mask save/restore
-    const uint64_t me = (1ull << lane_id()) & vm;
-    __hip_atomic_fetch_or(b0, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_or(b1, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-    const uint64_t s = __hip_atomic_load(b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
-                       __hip_atomic_load(b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-    __hip_atomic_store(b0, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_store(b1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-    return s;
-  }
-};
-
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
 // points), like the reference.
-template <bool kWide, bool kGuard, class Src, class Tab, class Grp>
-__device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const Tab& tab, const Grp& grp,
+template <bool kWide, bool kGuard, class Src, class Tab>
+__device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const Tab& tab,
                                               uint8_t* __restrict__ out, int out_cap, int cap) {
   const uint32_t lane = lane_id();
   int op = 0;
@@ -313,13 +303,19 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         const bool lead = kb == 0 && t0 != 0;
         const uint32_t o3 = 3u * t0;
         const uint32_t k = kb + lane - o3;
-        const uint32_t pk = kb == 0 ? s - o3 + lane : search_pos<kWide>(s, k);
+        // kb is uniform: the first chunk's positions are consecutive (step 1),
+        // later chunks' k >= 61 take the closed form with no k == 0 case
+        uint32_t pk = s - o3 + lane, nx = pk + 1u;
+        if (kb != 0) {
+          pk = search_pos_nz<kWide>(s, k);
+          nx = pk + ((63u + k) >> 6);
+        }
         // valid lanes (lz4.cc:510), as a compare straight into a lane mask
-        uint64_t vm = __builtin_amdgcn_uicmp(pk + (kb == 0 ? 1u : search_step(k)), mflimit, 37 /*ULE*/);
+        uint64_t vm = __builtin_amdgcn_uicmp(nx, mflimit, 37 /*ULE*/);
         if (lead) vm = (vm | 5ull) & ~2ull;
         const bool valid = (vm >> lane) & 1ull;
         const uint32_t seq = RD32(min(pk, last4));
-        if (!kGuard) {                               // the pending sequence
+        if (!kGuard && kb == 0 && pe_total) {        // the pending sequence (first chunk only)
           const uint32_t j = lane;
           const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
           const uint32_t h = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
@@ -331,15 +327,9 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
           pe_total = 0;
         }
         const uint32_t h = hashp<kWide>(seq);
-        const uint32_t told = tab.get(h);
-        // lanes of this chunk whose iteration hashes to the same slot
-        const uint64_t same = grp.same(h, valid, vm);
-        const uint64_t below = same & mask_lt(lane);
-        uint32_t refk = told;
-        if (below) {                                 // reference = the nearest earlier same-slot lane
-          const uint32_t jb = 63u - (uint32_t)__builtin_clzll(below);
-          refk = kb == 0 ? s - o3 + jb : search_pos<kWide>(s, kb + jb - o3);
-        }
+        // get + put of every valid lane at once, in lane order: refk is the
+        // entry as the sequential loop's get at this iteration reads it
+        const uint32_t refk = tab.xchg(h, pk, valid);
         // byU32 adds the distance check (lz4.cc:526, 614); byU16 sizes never need it
         // the lanes whose reference matches (lz4.cc:527, 610-616), as a
         // compare straight into a lane mask (a ballot of a bool would be
@@ -348,16 +338,18 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
         if (mm) {
           const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
-          const uint64_t later = same & ~mask_le(lane) & mask_le(ks);
-          if (valid && lane <= ks && later == 0) tab.put(h, pk);   // lz4.cc:526, 608
           ip = readlane(pk, ks);
           ref = readlane(refk, ks);
+          // undo the puts of the lanes after ks (the sequential loop stops at
+          // ks): per slot, the lowest such lane holds the entry as lanes <= ks
+          // left it -- its refk is a position <= ip (positions grow with the
+          // lane; entries from before the chunk are smaller still)
+          if (valid && lane > ks && refk <= ip) tab.restore(h, refk);
           catchup = !(lead && ks == 2u);
           found = true;
           break;
         }
         if ((vm | (lead ? 2ull : 0ull)) != ~0ull) break;   // ran past mflimit: last literals
-        if (valid && (same & ~mask_le(lane)) == 0) tab.put(h, pk);
       }
       if (!found) break;
 
@@ -370,13 +362,15 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
 #endif
         const uint32_t rem = matchlimit - (ip + kMinMatch);
-        const bool cl = lane < lim, ml_in = lane < rem;
+        const uint64_t clm = __builtin_amdgcn_uicmp(lane, lim, 36 /*ULT*/);   // lanes < lim
+        const uint64_t mlm = __builtin_amdgcn_uicmp(lane, rem, 36 /*ULT*/);   // lanes < rem
+        const bool cl = (clm >> lane) & 1ull, ml_in = (mlm >> lane) & 1ull;
         const uint32_t a0 = src.u8(cl ? ip - 1u - lane : 0u), b0 = src.u8(cl ? ref - 1u - lane : 0u);
         const uint32_t a1 = src.u8(ml_in ? ip + kMinMatch + lane : 0u);
         const uint32_t b1 = src.u8(ml_in ? ref + kMinMatch + lane : 0u);
         // compares straight into lane masks; lanes past lim / rem vote false
-        c = first_zero(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & (lim >= 64u ? ~0ull : mask_lt(lim)));
-        ml = first_zero(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & (rem >= 64u ? ~0ull : mask_lt(rem)));
+        c = first_zero(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & clm);
+        ml = first_zero(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
         if (c == 64u) {
 #pragma unroll 1
           for (;;) {
@@ -417,8 +411,21 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
       }
       const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
-      const uint32_t nl1 = run_bytes(lit), nm1 = run_bytes(ml);
-      const uint32_t remL = run_last(lit, nl1), remM = run_last(ml, nm1);   // < 255 each
+      uint32_t nl1, nm1, remL, remM;                 // remL/remM < 255 each
+      if (max(lit, ml) < 270u) {
+        // at most one run byte each (almost every sequence): (n+241)>>8 is
+        // (n >= 15), the byte n-15; without a run its "last byte" index falls
+        // on a byte of higher precedence, so any 8-bit value does
+        nl1 = (lit + 241u) >> 8;
+        nm1 = (ml + 241u) >> 8;
+        remL = (lit - 15u) & 255u;
+        remM = (ml - 15u) & 255u;
+      } else {
+        nl1 = run_bytes(lit);
+        nm1 = run_bytes(ml);
+        remL = run_last(lit, nl1);
+        remM = run_last(ml, nm1);
+      }
       const uint32_t ea = 1u + nl1;
       const uint32_t etot = ea + lit + 2u + nm1;
       if (!kGuard && etot <= 64u) {
@@ -514,9 +521,7 @@ __device__ __forceinline__ T sload(const T* p, uint32_t i) {
 // kFrame = true : CompressorLZ4::Compress per value; the slot must hold
 //   8 + compress_bound(S) bytes; frame_len[v] = frame bytes, ret[v] = 0 or -1.
 //
-// kBins (kSmall only): same-slot grouping through LDS bins (BinGroup, placed
-// after the value) instead of 13 ballots per search chunk.
-template <bool kFrame, bool kSmall, bool kBins>
+template <bool kFrame, bool kSmall>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
@@ -524,11 +529,10 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
     int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
     uint32_t cls, uint32_t nq) {
-  static_assert(kSmall || !kBins, "bins sit after the fixed 4 KiB value region");
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
   // kSmall: a fixed LDS layout, so every LDS address is a constant offset (a
   // dynamic allocation's base costs a v_add per address)
-  constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u + (kBins ? BinGroup::kBytes : 0u) : 16u;
+  constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u : 16u;
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
   uint8_t* const smem = kSmall ? smem_s : smem_d;
@@ -538,20 +542,14 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   uint8_t* s_in = smem + kTabBytes;      // value bytes [0, S), 16B-aligned
   const uint4 z4 = make_uint4(0, 0, 0, 0);
 
-  using Tab = typename std::conditional<kSmall, Table12, Table<false>>::type;
+  using Tab = typename std::conditional<kSmall, Table12, Table16>::type;
   Tab tab;
   if constexpr (kSmall) tab = Table12{smem, smem + 8192u};
-  else tab = Table<false>{tab16, 0u};
-  using Grp = typename std::conditional<kBins, BinGroup, BallotGroup<13>>::type;
-  Grp grp{};
-  if constexpr (kBins) grp.b = reinterpret_cast<uint64_t*>(smem + kTabBytes + 4096u);
+  else tab = Table16{tab16};
   if (kSmall) {
     for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(smem)[i] = z4;
   }
-  if (kBins) {
-    for (uint32_t i = lane; i < BinGroup::kBytes / 16u; i += 64u)
-      reinterpret_cast<uint4*>(smem + kTabBytes + 4096u)[i] = z4;
-  }
+
   // register prefetch (kSmall): the next value's realigned 16-byte chunks
   uint4 pa[kPrefetch], pb[kPrefetch];
   uint32_t p_head = 0, p_chunks = 0;
@@ -608,11 +606,11 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t bound = compress_bound(S);
     if (!kFrame) {
       const uint32_t cap = uni(dst_cap[v]);
-      const int r = cap < bound ? compress_block<false, true>(LdsSrc{s_in}, S, tab, grp, o, (int)cap, (int)cap)
-                                : compress_block<false, false>(LdsSrc{s_in}, S, tab, grp, o, (int)bound, (int)cap);
+      const int r = cap < bound ? compress_block<false, true>(LdsSrc{s_in}, S, tab, o, (int)cap, (int)cap)
+                                : compress_block<false, false>(LdsSrc{s_in}, S, tab, o, (int)bound, (int)cap);
       if (lane == 0) ret[v] = r;
     } else {
-      const int r = compress_block<false, false>(LdsSrc{s_in}, S, tab, grp, o + 8, (int)bound, (int)bound);
+      const int r = compress_block<false, false>(LdsSrc{s_in}, S, tab, o + 8, (int)bound, (int)bound);
       if (r <= 0) {                              // compressor.cc:31-34
         if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
       } else {
@@ -642,9 +640,9 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 }
 
 // LDS bytes a launch needs for values up to max_len bytes.
-size_t compress_lds_bytes(uint32_t max_len, bool bins) {
-  // 16 KiB: 10 per CU; with the grouping bins 17.5 KiB: 9 per CU
-  if (max_len <= kSmallMax) return kTable12Bytes + kSmallMax + (bins ? BinGroup::kBytes : 0u);
+size_t compress_lds_bytes(uint32_t max_len) {
+  // 16 KiB: 10 per CU
+  if (max_len <= kSmallMax) return kTable12Bytes + kSmallMax;
   return kTableBytes + (((size_t)max_len + 15u) & ~(size_t)15u);
 }
 
@@ -654,7 +652,7 @@ size_t compress_lds_bytes(uint32_t max_len, bool bins) {
 // 1 MB (util/options.h:171), so whole parts land here.  The value is read in
 // place from global memory (L2), the 16 KiB table lives in LDS; one wave per
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
-template <bool kFrame, bool kWide, bool kBins>
+template <bool kFrame, bool kWide>
 __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
@@ -666,19 +664,12 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   // arbitration over the small classes' waves that fill the GPU beside them
   if (prio) __builtin_amdgcn_s_setprio(2);
   __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
-  __shared__ __attribute__((aligned(16))) uint64_t bins_s[kBins ? BinGroup::kBytes / 8u : 1u];
   const uint32_t lane = lane_id();
   // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
-  using Tab = typename std::conditional<kWide, Table32, Table<false>>::type;
+  using Tab = typename std::conditional<kWide, Table32, Table16>::type;
   Tab tab;
   if constexpr (kWide) tab = Table32{tab32};
-  else tab = Table<false>{reinterpret_cast<uint16_t*>(tab32), 0u};
-  using Grp = typename std::conditional<kBins, BinGroup, BallotGroup<kWide ? 12 : 13>>::type;
-  Grp grp{};
-  if constexpr (kBins) {
-    grp.b = bins_s;
-    for (uint32_t i = lane; i < BinGroup::kBytes / 8u; i += 64u) bins_s[i] = 0ull;
-  }
+  else tab = Table16{reinterpret_cast<uint16_t*>(tab32)};
   bool direct_done = false;
 #pragma unroll 1
   for (;;) {
@@ -710,12 +701,12 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
         const uint32_t cap = uni(dst_cap[v]);
         int r = 0;
         if (bound != 0)
-          r = cap < bound ? compress_block<kWide, true>(GlobalSrc{g}, S, tab, grp, o, (int)cap, (int)cap)
-                          : compress_block<kWide, false>(GlobalSrc{g}, S, tab, grp, o, (int)bound, (int)cap);
+          r = cap < bound ? compress_block<kWide, true>(GlobalSrc{g}, S, tab, o, (int)cap, (int)cap)
+                          : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o, (int)bound, (int)cap);
         if (lane == 0) ret[v] = r;
       } else {
         const int r =
-            bound == 0 ? 0 : compress_block<kWide, false>(GlobalSrc{g}, S, tab, grp, o + 8, (int)bound, (int)bound);
+            bound == 0 ? 0 : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o + 8, (int)bound, (int)bound);
         if (r <= 0) {                                             // compressor.cc:31-34
           if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
         } else {
@@ -760,12 +751,12 @@ __global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n
   }
 }
 
-template <bool F, bool Sm, bool Bn = false>
+template <bool F, bool Sm>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0) {
-  auto kern = lz4_compress_kernel<F, Sm, Bn>;
+  auto kern = lz4_compress_kernel<F, Sm>;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t* work = nullptr;
   hipError_t e = launch_counter(st, n, grid, &work);
@@ -781,12 +772,7 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                              uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst, const uint64_t* dst_off,
                              const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret,
                              const uint32_t* census = nullptr, uint32_t cls = 0) {
-  // KDB_LZ4_BIGGROUP=bins|ballot: same-slot grouping of the in-place kernels
-  static const bool bins = [] {
-    const char* g = getenv("KDB_LZ4_BIGGROUP");
-    return g && strcmp(g, "bins") == 0;
-  }();
-  auto kern = bins ? lz4_compress_big_kernel<F, W, true> : lz4_compress_big_kernel<F, W, false>;
+  auto kern = lz4_compress_big_kernel<F, W>;
   static const uint32_t prio = env_prio();
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
   uint32_t* work = nullptr;
@@ -856,22 +842,11 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     if (e != hipSuccess) return e;
   }
   if (on[0]) {
-    // KDB_LZ4_GROUP=ballot: the 13-ballot grouping at 10 per CU (A/B diagnostic)
-    static const bool bins = [] {
-      const char* g = getenv("KDB_LZ4_GROUP");
-      return !(g && strcmp(g, "ballot") == 0);
-    }();
-    const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax, bins) bytes)
-    if (bins)
-      e = frame ? launch_one<true, true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off,
-                                               dst_cap, frame_len, ret, census, 0)
-                : launch_one<false, true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off,
-                                                dst_cap, frame_len, ret, census, 0);
-    else
-      e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                         frame_len, ret, census, 0)
-                : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                          frame_len, ret, census, 0);
+    const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
+    e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                       frame_len, ret, census, 0)
+              : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                        frame_len, ret, census, 0);
     if (e != hipSuccess) return e;
   }
   // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
@@ -879,7 +854,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
   if (on[1]) {
     const uint32_t top = min(max_len, hi[1]);
-    const size_t lds = compress_lds_bytes(top, false);
+    const size_t lds = compress_lds_bytes(top);
     e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
                                         dst_cap, frame_len, ret, census, 1)
               : launch_one<false, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,

@@ -19,6 +19,7 @@
 #   dropinfull the same with the whole test_db and client_emb (KDB_DROPIN_FULL=1)
 #   scalar     per-call latency of CompressorLZ4::Compress/Uncompress, drop-in vs reference
 #   ab:<NAME>=<VAL>  the quick headline line with one environment knob set
+#   var:<name> A/B of kingdb_amd/var/var_<name>.so (tools/ab.py, digest-gated)
 # Outputs land in gpurun_out/<tag>_*.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -82,6 +83,10 @@ for s in "$@"; do
           echo "$v $(cat ${O}_scalar_${v}_$sz.json)"
         done
       done ;;
+    var:*)    # A/B of a library build: kingdb_amd/var/var_<name>.so (tools/ab.py: timing + digest gate)
+      v=${s#var:}
+      timeout -k 10 300 python tools/ab.py kingdb_amd/var/var_$v.so --mixed > "${O}_var_$v.txt" 2>&1 || fail "var $v" $? "${O}_var_$v.txt"
+      cat "${O}_var_$v.txt" ;;
     ab:*)
       kv=${s#ab:}
       env "$kv" timeout -k 10 300 python bench.py --no-cpu-baseline > "${O}_ab_${kv}.json" 2> "${O}_ab.err" || fail "ab $kv" $? "${O}_ab.err"
