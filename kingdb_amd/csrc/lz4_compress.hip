@@ -84,8 +84,17 @@ __device__ __forceinline__ uint32_t hashp(uint32_t seq) { return (seq * 26544357
 // mskor: D = (D & ~mask) | data, on the dword holding the slot's field; a
 // lane with on = false passes mask 0 AND data 0 (no change) and still reads.
 
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// LDS byte offset of a (generic) pointer into LDS, made opaque so the
+// compiler keeps it in an SGPR instead of redoing the generic-to-LDS
+// conversion (a null test and a select) at every use inside the parse loop.
 __device__ __forceinline__ uint32_t lds_off(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+  uint32_t o = (uint32_t)(uintptr_t)(const lds_u8*)p;
+  asm volatile("" : "+s"(o));
+  return o;
 }
 
 // Two masked-or exchanges with return, one wait: the compiler does not count
@@ -116,43 +125,48 @@ __device__ __forceinline__ void mskor(uint32_t a, uint32_t m, uint32_t d) {
 // values per CU (the parse is latency-bound: occupancy is speed).  Cleared per
 // value (12 x 16 B stores per lane).
 struct Table12 {
-  uint8_t* lo;
-  uint8_t* hi;
+  uint32_t lo_off, hi_off;   // LDS byte offsets of the two planes
+  __device__ Table12(uint8_t* l, uint8_t* h) : lo_off(lds_off(l)), hi_off(lds_off(h)) {}
+  __device__ Table12() : lo_off(0), hi_off(0) {}
   // get-then-put of every lane of the chunk, in lane order (see above)
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
     const uint32_t sl = (h & 3u) << 3, sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
     const uint32_t ml = on ? 0xffu << sl : 0u, mh = on ? 15u << sh : 0u;
     uint32_t ol, oh;
-    mskor_rtn2(lds_off(lo) + (h & ~3u), ml, ((p & 0xffu) << sl) & ml, ol, lds_off(hi) + ((h >> 1) & ~3u), mh,
+    mskor_rtn2(lo_off + (h & ~3u), ml, ((p & 0xffu) << sl) & ml, ol, hi_off + ((h >> 1) & ~3u), mh,
                (((p >> 8) & 15u) << sh) & mh, oh);
     return ((ol >> sl) & 0xffu) | (((oh >> sh) & 15u) << 8);
   }
   __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const {
-    lo[h] = (uint8_t)v;
+    ((lds_u8*)(uintptr_t)lo_off)[h] = (uint8_t)v;
     const uint32_t sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
-    mskor(lds_off(hi) + ((h >> 1) & ~3u), 15u << sh, ((v >> 8) & 15u) << sh);
+    mskor(hi_off + ((h >> 1) & ~3u), 15u << sh, ((v >> 8) & 15u) << sh);
   }
 };
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
 
 // byU16 table, 8192 x u16 (values up to 65 546 bytes; positions < 65 536).
 struct Table16 {
-  uint16_t* t;
+  uint32_t off;
+  __device__ Table16(uint16_t* p) : off(lds_off(p)) {}
+  __device__ Table16() : off(0) {}
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
     const uint32_t sh = (h & 1u) << 4, m = on ? 0xffffu << sh : 0u;
-    const uint32_t o = mskor_rtn(lds_off(t) + ((h & ~1u) << 1), m, ((p & 0xffffu) << sh) & m);
+    const uint32_t o = mskor_rtn(off + ((h & ~1u) << 1), m, ((p & 0xffffu) << sh) & m);
     return (o >> sh) & 0xffffu;
   }
-  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { t[h] = (uint16_t)v; }
+  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { ((lds_u16*)(uintptr_t)off)[h] = (uint16_t)v; }
 };
 
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
 struct Table32 {
-  uint32_t* t;
+  uint32_t off;
+  __device__ Table32(uint32_t* p) : off(lds_off(p)) {}
+  __device__ Table32() : off(0) {}
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
-    return mskor_rtn(lds_off(t) + (h << 2), on ? 0xffffffffu : 0u, on ? p : 0u);
+    return mskor_rtn(off + (h << 2), on ? 0xffffffffu : 0u, on ? p : 0u);
   }
-  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { t[h] = v; }
+  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { ((lds_u32*)(uintptr_t)off)[h] = v; }
 };
 
 // Value bytes staged in LDS (byte i at p[i]).
@@ -295,63 +309,65 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
     for (;;) {
       pf = src.prefetch(s, S, pf);
       // ================= search (lz4.cc:494-527), 64 iterations per step
-      uint32_t ip = 0, ref = 0;
-      bool found = false, catchup = true;
+      // (the loop exits with the chunk that matched; a chunk that runs past
+      // mflimit without a match goes to the last literals)
+      uint32_t kb = 0, pk, refk, h;
+      uint64_t mm, vm;
+      bool lead;
 #pragma unroll 1
-      for (uint32_t kb = 0;; kb += 64u) {
+      for (;;) {
         // positions: step(k) = 1 for k <= 64, so the first chunk is s-o3+lane
-        const bool lead = kb == 0 && t0 != 0;
+        lead = kb == 0 && t0 != 0;
         const uint32_t o3 = 3u * t0;
         const uint32_t k = kb + lane - o3;
         // kb is uniform: the first chunk's positions are consecutive (step 1),
         // later chunks' k >= 61 take the closed form with no k == 0 case
-        uint32_t pk = s - o3 + lane, nx = pk + 1u;
+        pk = s - o3 + lane;
+        uint32_t nx = pk + 1u;
         if (kb != 0) {
           pk = search_pos_nz<kWide>(s, k);
           nx = pk + ((63u + k) >> 6);
         }
         // valid lanes (lz4.cc:510), as a compare straight into a lane mask
-        uint64_t vm = __builtin_amdgcn_uicmp(nx, mflimit, 37 /*ULE*/);
+        vm = __builtin_amdgcn_uicmp(nx, mflimit, 37 /*ULE*/);
         if (lead) vm = (vm | 5ull) & ~2ull;
-        const bool valid = (vm >> lane) & 1ull;
+        const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
         const uint32_t seq = RD32(min(pk, last4));
         if (!kGuard && kb == 0 && pe_total) {        // the pending sequence (first chunk only)
           const uint32_t j = lane;
           const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
-          const uint32_t h = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
+          const uint32_t hb = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
           const uint32_t t = j == pe_b ? (pe_w1 & 255u)
                            : j == pe_b + 1u ? (pe_w1 >> 8)
                            : (j + 1u == pe_total ? (pe_w0 >> 16) : 255u);
-          const uint32_t val = j < pe_a ? h : (j < pe_b ? lb : t);
+          const uint32_t val = j < pe_a ? hb : (j < pe_b ? lb : t);
           if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
           pe_total = 0;
         }
-        const uint32_t h = hashp<kWide>(seq);
+        h = hashp<kWide>(seq);
         // get + put of every valid lane at once, in lane order: refk is the
         // entry as the sequential loop's get at this iteration reads it
-        const uint32_t refk = tab.xchg(h, pk, valid);
-        // byU32 adds the distance check (lz4.cc:526, 614); byU16 sizes never need it
+        refk = tab.xchg(h, pk, valid);
         // the lanes whose reference matches (lz4.cc:527, 610-616), as a
         // compare straight into a lane mask (a ballot of a bool would be
-        // materialised in a VGPR and compared again)
-        uint64_t mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm & (lead ? ~1ull : ~0ull);
+        // materialised in a VGPR and compared again); byU32 adds the
+        // distance check (lz4.cc:526, 614), byU16 sizes never need it
+        mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm & (lead ? ~1ull : ~0ull);
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
-        if (mm) {
-          const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
-          ip = readlane(pk, ks);
-          ref = readlane(refk, ks);
-          // undo the puts of the lanes after ks (the sequential loop stops at
-          // ks): per slot, the lowest such lane holds the entry as lanes <= ks
-          // left it -- its refk is a position <= ip (positions grow with the
-          // lane; entries from before the chunk are smaller still)
-          if (valid && lane > ks && refk <= ip) tab.restore(h, refk);
-          catchup = !(lead && ks == 2u);
-          found = true;
-          break;
-        }
-        if ((vm | (lead ? 2ull : 0ull)) != ~0ull) break;   // ran past mflimit: last literals
+        // one exit: a match, or the chunk ran past mflimit (last literals)
+        if (mm || (vm | (lead ? 2ull : 0ull)) != ~0ull) break;
+        kb += 64u;
       }
-      if (!found) break;
+      if (!mm) break;
+      const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
+      uint32_t ip = readlane(pk, ks);
+      uint32_t ref = readlane(refk, ks);
+      // undo the puts of the lanes after ks (the sequential loop stops at ks):
+      // per slot, the lowest such lane holds the entry as lanes <= ks left it
+      // -- its refk is a position <= ip (positions grow with the lane; entries
+      // from before the chunk are smaller still)
+      if (__builtin_amdgcn_inverse_ballot_w64(vm) && lane > ks && refk <= ip) tab.restore(h, refk);
+      const bool catchup = !(lead && ks == 2u);   // a lane-2 match is _next_match
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml;
@@ -362,12 +378,14 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
         const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
 #endif
         const uint32_t rem = matchlimit - (ip + kMinMatch);
+        // the reads go out first (addresses clamped into the value, lanes
+        // past lim / rem read something harmless); the masks are built while
+        // they are in flight
+        const uint32_t a0 = src.u8(min(ip - 1u - lane, S - 1u)), b0 = src.u8(min(ref - 1u - lane, S - 1u));
+        const uint32_t a1 = src.u8(min(ip + kMinMatch + lane, S - 1u));
+        const uint32_t b1 = src.u8(min(ref + kMinMatch + lane, S - 1u));
         const uint64_t clm = __builtin_amdgcn_uicmp(lane, lim, 36 /*ULT*/);   // lanes < lim
         const uint64_t mlm = __builtin_amdgcn_uicmp(lane, rem, 36 /*ULT*/);   // lanes < rem
-        const bool cl = (clm >> lane) & 1ull, ml_in = (mlm >> lane) & 1ull;
-        const uint32_t a0 = src.u8(cl ? ip - 1u - lane : 0u), b0 = src.u8(cl ? ref - 1u - lane : 0u);
-        const uint32_t a1 = src.u8(ml_in ? ip + kMinMatch + lane : 0u);
-        const uint32_t b1 = src.u8(ml_in ? ref + kMinMatch + lane : 0u);
         // compares straight into lane masks; lanes past lim / rem vote false
         c = first_zero(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & clm);
         ml = first_zero(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
@@ -544,8 +562,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 
   using Tab = typename std::conditional<kSmall, Table12, Table16>::type;
   Tab tab;
-  if constexpr (kSmall) tab = Table12{smem, smem + 8192u};
-  else tab = Table16{tab16};
+  if constexpr (kSmall) tab = Table12(smem, smem + 8192u);
+  else tab = Table16(tab16);
   if (kSmall) {
     for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(smem)[i] = z4;
   }
@@ -668,8 +686,8 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
   using Tab = typename std::conditional<kWide, Table32, Table16>::type;
   Tab tab;
-  if constexpr (kWide) tab = Table32{tab32};
-  else tab = Table16{reinterpret_cast<uint16_t*>(tab32)};
+  if constexpr (kWide) tab = Table32(tab32);
+  else tab = Table16(reinterpret_cast<uint16_t*>(tab32));
   bool direct_done = false;
 #pragma unroll 1
   for (;;) {

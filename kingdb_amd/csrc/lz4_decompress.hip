@@ -27,6 +27,18 @@
 
 namespace kdb_lz4 {
 
+// A uniform value moved to (and kept in) a VGPR: the compiler treats inline
+// asm VGPR results as divergent, so arithmetic on it stays on the vector unit
+// instead of the CU's single scalar unit.
+__device__ __forceinline__ int vgpr(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t vgpr(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // 256-byte window over the staged block (LDS byte coordinates).
 struct Window {
   const uint32_t* w32;   // LDS buffer as dwords
@@ -76,70 +88,81 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
     if (have_q == 0) q = wd.get4(in_off + (uint32_t)ip);
     have_q = 0;
     {
-      // Fast path: a sequence that is not the last, with at most one length
+      // Fast path: sequences that are not the last, with at most one length
       // byte per run, <= 60 literals and no error.  One 64-lane load of the
       // literals also yields the offset, the match-length byte and the next
       // token (v_readlane), instead of scalar window reads.  Anything else --
-      // and every error, so its exact code -- goes through the general path
-      // below from the same token.
-      // Every scalar instruction counts here (the decoder issues about one per
-      // CU cycle), so the bounds are folded into one "far from both ends"
-      // test per sequence -- ip <= far_ip, op <= far_op make the not-last
-      // and output checks of any fast sequence true (lit <= 60, mlen <= 273)
-      // -- and the rest are sign bits of plain integer expressions, one
-      // compare per group, not chains of 64-bit lane-mask selects.
-      const int tk = (int)(q & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((q >> 8) & 0xffu);
-      const int lx = (ln + 1) >> 4;                               // a literal-length byte follows
-      const int xl = b1 & -lx;                                    // its value, or 0
-      const int lit = ln + xl;                                    // <= 60 iff !lx || b1 <= 45
-      if (((far_ip - ip) | (far_op - op) | (45 - xl)) >= 0) {
-        const int ls = ip + 1 + lx;
-        const int opl = op + lit;
+      // and every error, so its exact code -- leaves the loop and goes
+      // through the general path below from the same token.
+      //
+      // The decoder is bound by the CU's one scalar unit (about one scalar
+      // instruction per CU cycle with ~19 waves per CU), while the vector
+      // units idle, so this loop keeps its uniform state -- ip, op, the
+      // token word and the length arithmetic -- in VGPRs (vgpr(): every lane
+      // holds the same value) and only the loop and copy decisions go
+      // through the scalar unit (readfirstlane + one compare).  The bounds
+      // are folded into one "far from both ends" test per sequence -- ip <=
+      // far_ip, op <= far_op make the not-last and output checks of any fast
+      // sequence true (lit <= 60, mlen <= 273) -- and the rest are sign bits
+      // of plain integer expressions.
+      int vip = vgpr(ip), vop = vgpr(op);
+      uint32_t vq = vgpr(q);
+#pragma unroll 1
+      for (;;) {
+        const int tk = (int)(vq & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((vq >> 8) & 0xffu);
+        const int lx = (ln + 1) >> 4;                             // a literal-length byte follows
+        const int xl = b1 & -lx;                                  // its value, or 0
+        const int lit = ln + xl;                                  // <= 60 iff !lx || b1 <= 45
+        if (unii((far_ip - vip) | (far_op - vop) | (45 - xl)) < 0) break;
+        const int ls = vip + 1 + lx;
+        const int opl = vop + lit;
         // lane i holds the block's 4 bytes from ls + i: byte 0 is literal i,
         // and one readlane gives the offset + match-length byte, another the
         // next token and the byte after it
         const uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
-        const uint32_t w = readlane(v, (uint32_t)lit);
+        const uint32_t w = vgpr(readlane(v, (uint32_t)unii(lit)));
         const int e = (int)((w >> 16) & 0xffu);
         const int off = (int)(w & 0xffffu);
         const int mx = (mn + 1) >> 4;                             // a match-length byte follows
         const int xm = e & -mx;
         const int mlen = mn + xm + (int)kMinMatch;
-        if (((opl - off) | (254 - xm)) >= 0) {                    // ref >= 0; one match-length byte
-          out[op + (int)lane] = (uint8_t)v;        // lz4.cc:947 (lanes past lit: not-yet-produced output)
-          const uint32_t nt = (uint32_t)(lit + 2 + mx);             // next token's lane (<= 63)
-          q = readlane(v, nt);
-          have_q = 1;
-          ip = ls + lit + 2 + mx;
-          const int ref = opl - off;
-          asm volatile("" ::: "memory");
-          if (off < min(mlen, 64)) {
-            if (off > 0) {                          // periodic (see the general path)
-              const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-              const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+        if (unii((opl - off) | (254 - xm)) < 0) break;          // ref >= 0; one match-length byte
+        out[vop + (int)lane] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
+        const int nt = lit + 2 + mx;                              // next token's lane (<= 63)
+        vq = vgpr(readlane(v, (uint32_t)unii(nt)));
+        vip = ls + nt;
+        const int ref = opl - off;
+        asm volatile("" ::: "memory");
+        if (unii(off - min(mlen, 64)) < 0) {
+          if (unii(off) > 0) {                    // periodic (see the general path)
+            const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+            const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+            const int steps = unii(mlen);
 #pragma unroll 1
-              for (int i = 0; i < mlen; i += 64) {
-                const uint8_t b = out[ref + i + rr];
-                out[opl + i + (int)lane] = b;
-              }
-            }
-          } else {
-            // the first 64-byte step unconditionally (mlen >= 4), the rest only for long matches
-            const uint8_t b0 = out[ref + (int)lane];
-            out[opl + (int)lane] = b0;
-            asm volatile("" ::: "memory");
-#pragma unroll 1
-            for (int i = 64; i < mlen; i += 64) {
-              const uint8_t b = out[ref + i + (int)lane];
+            for (int i = 0; i < steps; i += 64) {
+              const uint8_t b = out[ref + i + rr];
               out[opl + i + (int)lane] = b;
-              asm volatile("" ::: "memory");
             }
           }
+        } else {
+          // the first 64-byte step unconditionally (mlen >= 4), the rest only for long matches
+          const uint8_t b0 = out[ref + (int)lane];
+          out[opl + (int)lane] = b0;
           asm volatile("" ::: "memory");
-          op = opl + mlen;
-          continue;
+          const int steps = unii(mlen);
+#pragma unroll 1
+          for (int i = 64; i < steps; i += 64) {
+            const uint8_t b = out[ref + i + (int)lane];
+            out[opl + i + (int)lane] = b;
+            asm volatile("" ::: "memory");
+          }
         }
+        asm volatile("" ::: "memory");
+        vop = opl + mlen;
       }
+      ip = unii(vip);
+      op = unii(vop);
+      q = (uint32_t)unii((int)vq);
     }
     const uint32_t token = q & 0xffu;
     ip++;

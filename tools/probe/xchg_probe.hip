@@ -20,7 +20,7 @@ __global__ void run(const uint32_t* slot, const uint32_t* pos, const uint32_t* v
   const uint32_t lane = threadIdx.x;
   for (uint32_t i = lane; i < kTable12Bytes; i += 64) t[i] = 0;
   __syncthreads();
-  Table12 tab{t, t + 8192};
+  Table12 tab(t, t + 8192);
   for (uint32_t c = 0; c < trials; c++) {
     const uint32_t h = slot[c * 64 + lane], p = pos[c * 64 + lane];
     const bool valid = val[c * 64 + lane] != 0;
