@@ -174,13 +174,15 @@ struct LdsSrc {
   const uint8_t* p;
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
   __device__ __forceinline__ uint32_t rd32(uint32_t i) const { return lds_rd32(p, i); }
-  __device__ __forceinline__ uint32_t prefetch(uint32_t, uint32_t, uint32_t) const { return 0u; }
+  __device__ __forceinline__ void step(uint32_t) {}
 };
 
 // Value bytes read in place from global memory (any alignment).  An aligned
 // dword never lies on a page no needed byte lies on, so the reads cannot fault.
 struct GlobalSrc {
   const uint8_t* g;
+  uint32_t S;
+  uint32_t keep;   // the frontier touch in flight (see step)
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return g[i]; }
   __device__ __forceinline__ uint32_t rd32(uint32_t i) const {
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3u);
@@ -189,29 +191,32 @@ struct GlobalSrc {
   }
   // Touches the 256 bytes from p + 256 (one aligned dword per lane, clamped
   // into the value) so the search frontier is in L1/L2 before it is parsed;
-  // `keep` is the previous call's dword, consumed here -- one sequence later,
-  // when it has long arrived -- so the compiler keeps the load.
-#ifndef KDB_PF_AHEAD
-#define KDB_PF_AHEAD 256u
-#endif
-#ifndef KDB_PF_DW
-#define KDB_PF_DW 1u
-#endif
-  __device__ __forceinline__ uint32_t prefetch(uint32_t p, uint32_t S, uint32_t keep) const {
-#ifdef KDB_PF_OFF
-    return 0u;
-#else
+  // the previous touch's dword is consumed here -- one sequence later, when
+  // it has long arrived -- so the compiler keeps the load.
+  __device__ __forceinline__ void step(uint32_t p) {
     asm volatile("" ::"v"(keep));
-    uint32_t x = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < KDB_PF_DW; ++k) {
-      const uint32_t a = min(p + KDB_PF_AHEAD + 256u * k + 4u * lane_id(), S - 1u);
-      x ^= *reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(g + a) & ~(uintptr_t)3);
-    }
-    return x;
-#endif
+    const uint32_t a = min(p + 256u + 4u * lane_id(), S - 1u);
+    keep = *reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(g + a) & ~(uintptr_t)3);
   }
 };
+
+// out chunk = bytes [sh, sh+16) of the 32 bytes (a, b); sh in 0..15 (uniform)
+__device__ __forceinline__ uint4 funnel16(const uint4& a, const uint4& b, uint32_t sh) {
+  if (sh == 0) return a;
+  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  const uint32_t q = sh >> 2, r = sh & 3u;
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t lo = w[k], hi = w[k + 1];
+    // select w[k+q], w[k+q+1] with a uniform q (0..3)
+    if (q == 1) { lo = w[k + 1]; hi = w[k + 2]; }
+    else if (q == 2) { lo = w[k + 2]; hi = w[k + 3]; }
+    else if (q == 3) { lo = w[k + 3]; hi = w[k + 4]; }
+    o[k] = __builtin_amdgcn_alignbyte(hi, lo, r);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
 
 // Output: bytes go straight to HBM at out[0..).  kGuard (LZ4_compress_limitedOutput
 // with a caller cap below the bound): never write at or past out_cap -- the
@@ -270,7 +275,7 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
 // points), like the reference.
 template <bool kWide, bool kGuard, class Src, class Tab>
-__device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const Tab& tab,
+__device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& tab,
                                               uint8_t* __restrict__ out, int out_cap, int cap) {
   const uint32_t lane = lane_id();
   int op = 0;
@@ -305,9 +310,8 @@ __device__ __forceinline__ int compress_block(const Src& src, uint32_t S, const 
     // _next_match: no catch-up, no literals.
     uint32_t s = 1;                                         // lz4.cc:487
     uint32_t t0 = 0;                                        // 1: the first chunk is a lead chunk
-    uint32_t pf = 0;                                        // GlobalSrc: the frontier prefetch in flight
     for (;;) {
-      pf = src.prefetch(s, S, pf);
+      src.step(s);
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
       // mflimit without a match goes to the last literals)
@@ -495,24 +499,6 @@ constexpr uint32_t kSmallMax = 4096u;     // tagged table + register prefetch
 constexpr uint32_t kMidLdsMax = 8192u;    // LDS-staged values up to here, in place above
 constexpr uint32_t kPrefetch = 4u;        // output chunks per lane: 4096 / 16 / 64
 
-// out chunk = bytes [sh, sh+16) of the 32 bytes (a, b); sh in 0..15 (uniform)
-__device__ __forceinline__ uint4 funnel16(const uint4& a, const uint4& b, uint32_t sh) {
-  if (sh == 0) return a;
-  const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-  const uint32_t q = sh >> 2, r = sh & 3u;
-  uint32_t o[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    uint32_t lo = w[k], hi = w[k + 1];
-    // select w[k+q], w[k+q+1] with a uniform q (0..3)
-    if (q == 1) { lo = w[k + 1]; hi = w[k + 2]; }
-    else if (q == 2) { lo = w[k + 2]; hi = w[k + 3]; }
-    else if (q == 3) { lo = w[k + 3]; hi = w[k + 4]; }
-    o[k] = __builtin_amdgcn_alignbyte(hi, lo, r);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
 // Stages value bytes g[0 .. n) into LDS at offset 0 (16B-aligned), whatever
 // g's alignment: whole aligned 16-byte loads (an aligned chunk never crosses a
 // page, so the over-read cannot fault), realigned in registers.
@@ -624,11 +610,13 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint32_t bound = compress_bound(S);
     if (!kFrame) {
       const uint32_t cap = uni(dst_cap[v]);
-      const int r = cap < bound ? compress_block<false, true>(LdsSrc{s_in}, S, tab, o, (int)cap, (int)cap)
-                                : compress_block<false, false>(LdsSrc{s_in}, S, tab, o, (int)bound, (int)cap);
+      LdsSrc ls{s_in};
+      const int r = cap < bound ? compress_block<false, true>(ls, S, tab, o, (int)cap, (int)cap)
+                                : compress_block<false, false>(ls, S, tab, o, (int)bound, (int)cap);
       if (lane == 0) ret[v] = r;
     } else {
-      const int r = compress_block<false, false>(LdsSrc{s_in}, S, tab, o + 8, (int)bound, (int)bound);
+      LdsSrc ls{s_in};
+      const int r = compress_block<false, false>(ls, S, tab, o + 8, (int)bound, (int)bound);
       if (r <= 0) {                              // compressor.cc:31-34
         if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
       } else {
@@ -715,16 +703,17 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
       uint8_t* o = dst + dst_off[v];
       for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(0, 0, 0, 0);
       const uint32_t bound = compress_bound(S);                   // 0 past LZ4_MAX_INPUT_SIZE
+      GlobalSrc ws{g, S, 0u};
       if (!kFrame) {
         const uint32_t cap = uni(dst_cap[v]);
         int r = 0;
         if (bound != 0)
-          r = cap < bound ? compress_block<kWide, true>(GlobalSrc{g}, S, tab, o, (int)cap, (int)cap)
-                          : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o, (int)bound, (int)cap);
+          r = cap < bound ? compress_block<kWide, true>(ws, S, tab, o, (int)cap, (int)cap)
+                          : compress_block<kWide, false>(ws, S, tab, o, (int)bound, (int)cap);
         if (lane == 0) ret[v] = r;
       } else {
         const int r =
-            bound == 0 ? 0 : compress_block<kWide, false>(GlobalSrc{g}, S, tab, o + 8, (int)bound, (int)bound);
+            bound == 0 ? 0 : compress_block<kWide, false>(ws, S, tab, o + 8, (int)bound, (int)bound);
         if (r <= 0) {                                             // compressor.cc:31-34
           if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
         } else {

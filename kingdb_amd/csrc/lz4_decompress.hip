@@ -113,20 +113,23 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         const int lx = (ln + 1) >> 4;                             // a literal-length byte follows
         const int xl = b1 & -lx;                                  // its value, or 0
         const int lit = ln + xl;                                  // <= 60 iff !lx || b1 <= 45
-        if (unii((far_ip - vip) | (far_op - vop) | (45 - xl)) < 0) break;
         const int ls = vip + 1 + lx;
         const int opl = vop + lit;
         // lane i holds the block's 4 bytes from ls + i: byte 0 is literal i,
         // and one readlane gives the offset + match-length byte, another the
-        // next token and the byte after it
+        // next token and the byte after it.  The load goes out before the
+        // fast-path test (its address is inside the staged block plus the
+        // window slack for any token; a sequence that fails the test never
+        // uses it), so both tests are one scalar decision.
         const uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
-        const uint32_t w = vgpr(readlane(v, (uint32_t)unii(lit)));
+        const uint32_t w = readlane(v, (uint32_t)unii(lit) & 63u);   // offset, match-length byte
         const int e = (int)((w >> 16) & 0xffu);
         const int off = (int)(w & 0xffffu);
         const int mx = (mn + 1) >> 4;                             // a match-length byte follows
         const int xm = e & -mx;
         const int mlen = mn + xm + (int)kMinMatch;
-        if (unii((opl - off) | (254 - xm)) < 0) break;          // ref >= 0; one match-length byte
+        // far from both ends, <= 60 literals, ref >= 0, one match-length byte
+        if (unii((far_ip - vip) | (far_op - vop) | (45 - xl) | (opl - off) | (254 - xm)) < 0) break;
         out[vop + (int)lane] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
         const int nt = lit + 2 + mx;                              // next token's lane (<= 63)
         vq = vgpr(readlane(v, (uint32_t)unii(nt)));
@@ -422,71 +425,91 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
     if (have_q == 0) q = wd.get4((uint32_t)ip);
     have_q = 0;
     {
-      // decode_block's fast path, over the rings: the literal load reads the
-      // input ring (its mirror covers the wrap; ensure() staged 512 bytes past
-      // ip), stores are masked (ring slots past the run may still be match
-      // sources), and the match source must lie in the output ring.
-      const int tk = (int)(q & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((q >> 8) & 0xffu);
-      const int lx = (ln + 1) >> 4;
-      const int xl = b1 & -lx;
-      const int lit = ln + xl;
-      if (((far_ip - ip) | (far_op - op) | (45 - xl)) >= 0) {
-        const int ls = ip + 1 + lx;
-        const int opl = op + lit;
+      // decode_block's fast path, over the rings, on the vector unit like
+      // decode_block's (uniform state in VGPRs): the literal load reads the
+      // input ring (its mirror covers the wrap; the loop runs while 512
+      // bytes past ip are staged), stores are masked (ring slots past the
+      // run may still be match sources), and the match source must lie in
+      // the output ring.  A sequence whose next token sits on lane 63 (its
+      // second byte not loaded) ends the loop after it, q to be re-read.
+      const int lim_ip = min(far_ip, (int)in.filled - (int)kIMirror);
+      int vip = vgpr(ip), vop = vgpr(op);
+      uint32_t vq = vgpr(q);
+      int qok = 1;
+#pragma unroll 1
+      for (;;) {
+        const int tk = (int)(vq & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((vq >> 8) & 0xffu);
+        const int lx = (ln + 1) >> 4;
+        const int xl = b1 & -lx;
+        const int lit = ln + xl;
+        const int ls = vip + 1 + lx;
+        const int opl = vop + lit;
         const uint32_t v = in.lds[((uint32_t)ls & kIMask) + lane];
-        const int e = (int)readlane(v, (uint32_t)lit + 2u);
-        const int off = (int)(readlane(v, (uint32_t)lit) | (readlane(v, (uint32_t)lit + 1u) << 8));
+        const uint32_t l3 = (uint32_t)unii(lit) & 63u;
+        const int e = (int)readlane(v, (l3 + 2u) & 63u);
+        const int off = (int)(readlane(v, l3) | (readlane(v, (l3 + 1u) & 63u) << 8));
         const int mx = (mn + 1) >> 4;
         const int xm = e & -mx;
         const int mlen = mn + xm + (int)kMinMatch;
-        if (((opl - off) | (254 - xm) | ((int)kORing - off)) >= 0) {
-          if ((int)lane < lit) {
-            ring[(uint32_t)(op + (int)lane) & kOMask] = (uint8_t)v;
-            o[op + (int)lane] = (uint8_t)v;
-          }
-          const uint32_t nt = (uint32_t)(lit + 2 + mx);
-          q = readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8);
-          have_q = (int)(63u - nt);
-          ip = ls + lit + 2 + mx;
-          const int ref = opl - off;
-          asm volatile("" ::: "memory");
-          if (off < min(mlen, 64)) {
-            if (off > 0) {
-              const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-              const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+        if (unii((lim_ip - vip) | (far_op - vop) | (45 - xl) | (opl - off) | (254 - xm) | ((int)kORing - off)) < 0)
+          break;
+        if ((int)lane < lit) {
+          ring[(uint32_t)(vop + (int)lane) & kOMask] = (uint8_t)v;
+          o[vop + (int)lane] = (uint8_t)v;
+        }
+        const uint32_t nt = (uint32_t)unii(lit + 2 + mx);
+        vq = vgpr(readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8));
+        vip = ls + lit + 2 + mx;
+        const int ref = opl - off;
+        asm volatile("" ::: "memory");
+        const int steps = unii(mlen);
+        if (unii(off - min(mlen, 64)) < 0) {
+          if (unii(off) > 0) {
+            const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+            const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
 #pragma unroll 1
-              for (int i = 0; i < mlen; i += 64) {
-                const int j = i + (int)lane;
-                const uint8_t b = ring[(uint32_t)(ref + i + rr) & kOMask];
-                if (j < mlen) {
-                  ring[(uint32_t)(opl + j) & kOMask] = b;
-                  o[opl + j] = b;
-                }
-              }
-            } else {
-#pragma unroll 1
-              for (int i = 0; i < mlen; i += 64) {
-                const int j = i + (int)lane;
-                if (j < mlen) o[opl + j] = ring[(uint32_t)(opl + j) & kOMask];
-              }
-            }
-          } else {
-#pragma unroll 1
-            for (int i = 0; i < mlen; i += 64) {
+            for (int i = 0; i < steps; i += 64) {
               const int j = i + (int)lane;
-              const uint8_t b = ring[(uint32_t)(ref + j) & kOMask];
+              const uint8_t b = ring[(uint32_t)(ref + i + rr) & kOMask];
               if (j < mlen) {
                 ring[(uint32_t)(opl + j) & kOMask] = b;
                 o[opl + j] = b;
               }
-              asm volatile("" ::: "memory");
+            }
+          } else {
+#pragma unroll 1
+            for (int i = 0; i < steps; i += 64) {
+              const int j = i + (int)lane;
+              if (j < mlen) o[opl + j] = ring[(uint32_t)(opl + j) & kOMask];
             }
           }
-          asm volatile("" ::: "memory");
-          op = opl + mlen;
-          continue;
+        } else {
+#pragma unroll 1
+          for (int i = 0; i < steps; i += 64) {
+            const int j = i + (int)lane;
+            const uint8_t b = ring[(uint32_t)(ref + j) & kOMask];
+            if (j < mlen) {
+              ring[(uint32_t)(opl + j) & kOMask] = b;
+              o[opl + j] = b;
+            }
+            asm volatile("" ::: "memory");
+          }
+        }
+        asm volatile("" ::: "memory");
+        vop = opl + mlen;
+        if (nt >= 63u) {                      // the next token's second byte was not loaded
+          qok = 0;
+          break;
         }
       }
+      ip = unii(vip);
+      op = unii(vop);
+      q = (uint32_t)unii((int)vq);
+      if (!qok) {
+        // resume at the top: re-stage if needed, re-read the token
+        continue;
+      }
+      if (in.ensure((uint32_t)ip + kIMirror)) wd.invalidate();
     }
     const uint32_t token = q & 0xffu;
     ip++;
