@@ -51,12 +51,14 @@ __device__ __forceinline__ uint32_t rd32g(const uint8_t* p) {
 }
 
 // End of a value's walk
-constexpr uint32_t kEndDone = 0, kEndTail = 1, kEndError = 2;
+// kEndCap: the value's frames did not fit the launch's frame capacity (its
+// status is KDB_LZ4_VALUE_UNSUPPORTED, not an IOError: the bytes may be fine)
+constexpr uint32_t kEndDone = 0, kEndTail = 1, kEndError = 2, kEndCap = 3;
 
 struct ValueWalk {
   uint64_t tail_in, tail_out, tail_len;   // raw bytes copied after the frames
   uint32_t nframes;                       // frames found (decoded by the frame kernels)
-  uint32_t end;                           // kEndDone / kEndTail / kEndError
+  uint32_t end;                           // kEndDone / kEndTail / kEndError / kEndCap
 };
 
 // One walk; kFill writes the frame descriptors.
@@ -86,7 +88,7 @@ __device__ ValueWalk walk(const uint8_t* s, uint64_t avail, uint64_t svc, uint64
         if (fsz > avail - in) { w.end = kEndError; break; }
       }
       if (kFill) {
-        if (w.nframes >= frame_cap) { w.end = kEndError; break; }
+        if (w.nframes >= frame_cap) { w.end = kEndCap; break; }
         f_off[w.nframes] = base_in + in;
         f_avail[w.nframes] = (uint32_t)min(avail - in, (uint64_t)0xFFFFFFFFu);
         f_out[w.nframes] = out_base + o;
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(kFinishBlock) void get_finish_kernel(
     uint8_t* o = out + out_off[v];
     int32_t st = 0;
     uint64_t defined = 0;
-    if (f0 + w.nframes > frame_cap) {
+    if (w.end == kEndCap || f0 + w.nframes > frame_cap) {
       st = KDB_LZ4_VALUE_UNSUPPORTED;   // more frames than the launch's frame capacity
     } else {
       // frames in order: the first failure ends the value; a frame that decoded

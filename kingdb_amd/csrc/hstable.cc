@@ -639,10 +639,14 @@ int append_loop(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t
 template <class Land>
 int append_batch(kdb_hstable_writer* w, const uint64_t* entry_off, const uint32_t* entry_len, const uint64_t* hashed,
                  const uint32_t* kind, const int32_t* status, uint32_t n, Land land) {
+#ifdef KDB_LZ4_TUNING
   static const bool serial = [] {
     const char* e = getenv("KDB_HSTABLE_SERIAL");     // diagnostic: one thread, entry by entry
     return e && *e && *e != '0';
   }();
+#else
+  constexpr bool serial = false;
+#endif
   if (!serial && n >= kFastMin) {
     const int rc = append_fast(w, entry_off, entry_len, hashed, kind, status, n, land);
     if (rc != 1) return rc;

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <mutex>
+#include <functional>
 #include <unordered_map>
 
 namespace kdb_lz4 {
@@ -14,15 +15,33 @@ namespace kdb_lz4 {
 namespace {
 // Per-device pool of 512-byte counter slots (a WorkQueue's 8 counters, 64 B
 // apart).  A launch takes the next slot round-robin and zeroes it on its own
-// stream (a slot is reused only after 2048 later launches -- far more than
-// can be in flight).
+// stream.  Each slot carries an event recorded on the stream of its last user
+// (work_counter_release, after the launches that read it): a slot handed out
+// again -- 2048 launches later -- first waits for that event, so a slot is
+// never zeroed under a kernel still dequeuing from it, whatever the number of
+// streams and host threads.
 constexpr uint32_t kSlots = 2048, kSlotBytes = 512;
 struct Pool {
   uint8_t* base = nullptr;
   std::atomic<uint32_t> next{0};
+  hipEvent_t ev[kSlots] = {};
+  bool live[kSlots] = {};
+  std::mutex mu;               // guards ev/live
 };
 std::mutex g_mu;
 std::unordered_map<int, Pool*> g_pools;
+
+Pool* pool_of(uint8_t* ctr, uint32_t* slot) {
+  std::lock_guard<std::mutex> l(g_mu);
+  for (auto& kv : g_pools) {
+    Pool* p = kv.second;
+    if (p && ctr >= p->base && ctr < p->base + (size_t)kSlots * kSlotBytes) {
+      *slot = (uint32_t)((ctr - p->base) / kSlotBytes);
+      return p;
+    }
+  }
+  return nullptr;
+}
 }  // namespace
 
 hipError_t work_counter(hipStream_t st, uint32_t** ctr) {
@@ -44,10 +63,44 @@ hipError_t work_counter(hipStream_t st, uint32_t** ctr) {
     }
     p = slot;
   }
-  uint8_t* c = p->base + (size_t)(p->next.fetch_add(1) % kSlots) * kSlotBytes;
+  const uint32_t i = p->next.fetch_add(1) % kSlots;
+  {
+    std::lock_guard<std::mutex> l(p->mu);
+    if (p->live[i]) {                  // the slot's previous users must be done with it
+      e = hipEventSynchronize(p->ev[i]);
+      if (e != hipSuccess) return e;
+      p->live[i] = false;
+    }
+  }
+  uint8_t* c = p->base + (size_t)i * kSlotBytes;
   e = hipMemsetAsync(c, 0, kSlotBytes, st);
   *ctr = reinterpret_cast<uint32_t*>(c);
   return e;
+}
+
+// The launches that read `ctr` are all queued on `st` (or joined into it):
+// record the slot's fence there.
+hipError_t work_counter_release(hipStream_t st, uint32_t* ctr) {
+  if (!ctr) return hipSuccess;
+  uint32_t i = 0;
+  Pool* p = pool_of(reinterpret_cast<uint8_t*>(ctr), &i);
+  if (!p) return hipErrorInvalidValue;
+  std::lock_guard<std::mutex> l(p->mu);
+  hipError_t e = hipSuccess;
+  if (!p->ev[i] && (e = hipEventCreateWithFlags(&p->ev[i], hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventRecord(p->ev[i], st)) != hipSuccess) return e;
+  p->live[i] = true;
+  return hipSuccess;
+}
+
+long kdb_tune(const char* name, long dflt) {
+#ifdef KDB_LZ4_TUNING
+  const char* e = getenv(name);
+  return e && *e ? strtol(e, nullptr, 0) : dflt;
+#else
+  (void)name;
+  return dflt;
+#endif
 }
 
 hipError_t launch_counter(hipStream_t st, uint32_t n, uint32_t grid, uint32_t** ctr) {
@@ -66,43 +119,46 @@ uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
-  static const int cap = [] {
-    const char* e = getenv("KDB_LZ4_PER_CU");     // diagnostic: cap workgroups per CU
-    return e && *e ? atoi(e) : 0;
-  }();
+  static const int cap = (int)kdb_tune("KDB_LZ4_PER_CU", 0);   // cap workgroups per CU
   if (cap > 0 && per_cu > cap) per_cu = cap;
-  static const bool dbg = getenv("KDB_LZ4_DEBUG") != nullptr;
+  static const bool dbg = kdb_tune("KDB_LZ4_DEBUG", 0) != 0;
   if (dbg) fprintf(stderr, "persistent_grid: lds=%zu per_cu=%d cus=%d\n", lds, per_cu, cus);
   uint64_t slots = (uint64_t)per_cu * (uint64_t)cus;
-#ifdef KDB_ABL_GRID_MULT
-  slots *= KDB_ABL_GRID_MULT;   // diagnostic: oversubscribe the persistent grid
-#endif
   return (uint32_t)(n < slots ? n : slots);
 }
 
 // Fork/join of a second stream, so that size-class launches overlap: the
 // long-latency big-value class runs beside the small classes, and its tail
 // (the last few big values) no longer idles the rest of the GPU.  One
-// non-blocking stream and two events per host thread and device.
+// non-blocking stream and two events per host thread, device and CALLER
+// stream: batches a caller issues on different streams keep their own aux
+// streams, so one batch's big class never queues behind another's.
 namespace {
 struct Fork {
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
-thread_local std::unordered_map<int, Fork> t_fork;
+struct ForkKey {
+  int dev;
+  hipStream_t st;
+  bool operator==(const ForkKey& o) const { return dev == o.dev && st == o.st; }
+};
+struct ForkKeyHash {
+  size_t operator()(const ForkKey& k) const {
+    return std::hash<const void*>()(k.st) ^ (std::hash<int>()(k.dev) * 0x9e3779b97f4a7c15ull);
+  }
+};
+thread_local std::unordered_map<ForkKey, Fork, ForkKeyHash> t_fork;
 }  // namespace
 
 hipError_t fork_begin(hipStream_t st, hipStream_t* aux) {
-  static const bool off = [] {
-    const char* e = getenv("KDB_LZ4_NOFORK");     // diagnostic: classes in sequence on one stream
-    return e && *e && *e != '0';
-  }();
+  static const bool off = kdb_tune("KDB_LZ4_NOFORK", 0) != 0;   // classes in sequence on one stream
   *aux = st;
   if (off) return hipSuccess;
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  Fork& f = t_fork[dev];
+  Fork& f = t_fork[ForkKey{dev, st}];
   if (!f.aux) {
     if ((e = hipStreamCreateWithFlags(&f.aux, hipStreamNonBlocking)) != hipSuccess) return e;
     if ((e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming)) != hipSuccess) return e;
@@ -120,7 +176,7 @@ hipError_t fork_end(hipStream_t st, hipStream_t aux) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  Fork& f = t_fork[dev];
+  Fork& f = t_fork[ForkKey{dev, st}];
   if ((e = hipEventRecord(f.join, aux)) != hipSuccess) return e;
   return hipStreamWaitEvent(st, f.join, 0);
 }
@@ -131,10 +187,7 @@ hipError_t fork_end(hipStream_t st, hipStream_t aux) {
 // range vs 5.30 ms with eight (1 Mi x 4 KiB).  So: eight, unless overridden.
 uint32_t work_queues(uint32_t max_len) {
   (void)max_len;
-  static const int env = [] {
-    const char* e = getenv("KDB_LZ4_QUEUES");      // diagnostic: force 1 or 8 ranges
-    return e && *e ? atoi(e) : 0;
-  }();
+  static const int env = (int)kdb_tune("KDB_LZ4_QUEUES", 0);   // force 1 or 8 ranges
   if (env > 0) return (uint32_t)env;
   return 8u;   // kQueues (lz4_device.h)
 }
@@ -148,9 +201,6 @@ uint32_t claim_batch(uint32_t n, uint32_t grid) {
   return (uint32_t)b;
 }
 
-uint32_t env_prio() {
-  const char* e = getenv("KDB_LZ4_BIGPRIO");
-  return e && *e && *e != '0' ? 1u : 0u;
-}
+uint32_t env_prio() { return kdb_tune("KDB_LZ4_BIGPRIO", 0) != 0 ? 1u : 0u; }
 
 }  // namespace kdb_lz4

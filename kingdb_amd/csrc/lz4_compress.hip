@@ -6,28 +6,27 @@
 // (algorithm/compressor.cc:26-59).  Output is byte-identical to the reference.
 //
 // Persistent launch: one wavefront (workgroup of 64) per resident slot takes
-// values from a device-scope work counter, one value ahead.  LDS per
-// workgroup = the byU16 hash table (8192 x u16) + the value, realigned to
-// offset 0 while it is staged: 20 KiB for 4 KiB values, i.e. 8 resident
-// values per CU.  Every LDS read is clamped into that region.  For launches
-// whose values are all <= 4 KiB the table carries a 4-bit generation tag beside
-// each 12-bit position, so it is cleared once per 15 values instead of per
-// value (a stale tag reads as the zeroed slot, position 0 -- lz4.cc:669
-// semantics), and the next value is prefetched into registers while the
-// current one is parsed.  Each sequence's bytes (token, length runs, literals,
-// offset) are written straight to HBM by one wave-wide store per 64 bytes.
+// values from device-scope work counters, one value ahead.  Size classes
+// (launch_compress): values <= 4 KiB are staged in LDS next to a two-plane
+// 12-bit table (16 KiB per value, 10 values per CU) and the next value is
+// prefetched into registers while the current one is parsed; 4-8 KiB values
+// are staged next to a u16 table; larger values are read in place from
+// HBM/L2 with only the table (u16 for byU16, u32 for byU32) in LDS.  The
+// table is zeroed per value (lz4.cc:669: an empty slot reads as position 0).
+// Every LDS read is clamped into its region.  Each sequence's bytes (token,
+// length runs, literals, offset) are written straight to HBM by one
+// wave-wide byte store per 64 bytes.
 //
 // The greedy parse is sequential by definition; what is parallel is:
 //  * the search loop (lz4.cc:494-527): the positions it visits from a start
 //    `s` are a closed-form function of the iteration index (step =
 //    nb++ >> SKIPSTRENGTH), so 64 iterations are evaluated at once, one per
-//    lane.  An iteration's table read must see every earlier iteration's put:
-//    lanes with the same 13-bit hash are grouped with 13 ballots (bit-sliced
-//    match-any) and a lane takes its reference from the nearest lower lane of
-//    its group, else from the table as it stood before the chunk.  The first
-//    matching lane ends the chunk; only puts of lanes up to it are committed
-//    (the last lane of each group writes), exactly the table state the
-//    sequential loop would leave;
+//    lane.  Iteration k's table get must see every earlier iteration's put:
+//    one lane-ordered LDS exchange (ds_mskor_rtn_b32) per table plane does
+//    the get+put of all 64 iterations, each lane reading its slot as the
+//    lanes before it left it (see "hash tables" below).  The first matching
+//    lane ends the chunk; the puts of the lanes after it are undone, leaving
+//    exactly the table state of the sequential loop;
 //  * the catch-up loop (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued
 //    together: the match length after catching up c bytes is c + the length
 //    measured from the original position, so neither waits for the other;
@@ -245,7 +244,6 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   const uint32_t a = 1u + nl1;                                     // first literal byte
   const uint32_t b = a + lit;                                      // offset low byte
   const uint32_t total = has_match ? b + 2u + nm1 : b;
-#ifndef KDB_ABL_NO_EMIT
   // One pass per 64 bytes; every byte class is a compare-select: token,
   // 255-run bytes, remL, literals (one LDS byte read), offset, 255-run, remM.
   // Without a run its "last byte" index falls on a byte of higher precedence
@@ -260,13 +258,8 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
     const uint32_t h = j == 0 ? token : (j == remL_at ? remL : 255u);
     const uint32_t t = j == b ? (off & 255u) : j == b + 1u ? (off >> 8) : (j == remM_at ? remM : 255u);
     const uint32_t val = j < a ? h : (j < b ? lb : t);
-#ifdef KDB_ABL_SINK
-    asm volatile("" ::"v"(val), "v"(j < total ? 1u : 0u));
-#else
     if (j < total && (!kGuard || pos + (int)j < out_cap)) out[pos + (int)j] = (uint8_t)val;
-#endif
   }
-#endif
   return (int)total;
 }
 
@@ -287,11 +280,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
   uint32_t pe_a = 0, pe_b = 0, pe_total = 0, pe_w0 = 0, pe_w1 = 0;   // w0 = tok|remL<<8|remM<<16, w1 = off
 #define RD32(p) src.rd32(p)
 
-#ifdef KDB_ABL_NO_PARSE
-  if (S >= kMinLength && cap < 0) {
-#else
   if (S >= kMinLength) {                                    // lz4.cc:483
-#endif
     const uint32_t mflimit = S - kMfLimit;
     const uint32_t matchlimit = S - kLastLiterals;
     const uint32_t last4 = S - 4u;                          // highest position a u32 read may start
@@ -376,11 +365,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml;
       {
-#ifdef KDB_ABL_NO_CATCH
-        const uint32_t lim = 0u;
-#else
         const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
-#endif
         const uint32_t rem = matchlimit - (ip + kMinMatch);
         // the reads go out first (addresses clamped into the value, lanes
         // past lim / rem read something harmless); the masks are built while
@@ -601,9 +586,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       prefetch(vn);                  // the next value's loads fly while this one is parsed
     } else {
       stage_aligned(g, S, s_in);
-#ifndef KDB_ABL_NO_ZERO
       for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
-#endif
     }
     __syncthreads();
 
@@ -635,10 +618,8 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
       }
     }
     if (kSmall) {                                // a zeroed table per value (lz4.cc:669)
-#ifndef KDB_ABL_NO_ZERO
 #pragma unroll
       for (uint32_t k = 0; k < kTabBytes / 1024u; ++k) reinterpret_cast<uint4*>(smem)[lane + 64u * k] = z4;
-#endif
     }
     __syncthreads();
     v = vn;
@@ -771,7 +752,9 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap));
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return work_counter_release(st, work);
 }
 
 template <bool F, bool W>
@@ -788,7 +771,9 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, prio);
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return work_counter_release(st, work);
 }
 
 // One launch per size class that [min_len, max_len] (the launch's bounds on
@@ -804,10 +789,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   if (n == 0) return hipSuccess;
   if (min_len > max_len) min_len = 0;
   hipError_t e;
-  static const uint32_t mid_split = [] {
-    const char* v = getenv("KDB_LZ4_CSPLIT");
-    return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : kMidLdsMax;
-  }();
+  static const uint32_t mid_split = (uint32_t)kdb_tune("KDB_LZ4_CSPLIT", kMidLdsMax);
   const uint32_t b1 = min(max(mid_split, kSmallMax), k64KLimit - 1u);   // top of the LDS-staged class
   // class c covers lengths [lo[c], hi[c]]
   const uint32_t lo[4] = {0u, kSmallMax + 1u, b1 + 1u, k64KLimit};
@@ -868,7 +850,8 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                                          dst_cap, frame_len, ret, census, 1);
     if (e != hipSuccess) return e;
   }
-  return fork ? fork_end(st, aux) : hipSuccess;
+  if (fork && (e = fork_end(st, aux)) != hipSuccess) return e;
+  return work_counter_release(st, census);   // its readers are all joined into st by now
 }
 
 }  // namespace kdb_lz4

@@ -137,15 +137,18 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         const int ref = opl - off;
         asm volatile("" ::: "memory");
         if (unii(off - min(mlen, 64)) < 0) {
+          const int steps = unii(mlen);
           if (unii(off) > 0) {                    // periodic (see the general path)
             const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
             const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
-            const int steps = unii(mlen);
 #pragma unroll 1
             for (int i = 0; i < steps; i += 64) {
               const uint8_t b = out[ref + i + rr];
               out[opl + i + (int)lane] = b;
             }
+          } else {                                // offset 0: zeros (see the general path)
+#pragma unroll 1
+            for (int i = 0; i < steps; i += 64) out[opl + i + (int)lane] = 0;
           }
         } else {
           // the first 64-byte step unconditionally (mlen >= 4), the rest only for long matches
@@ -235,7 +238,13 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         const uint8_t b = out[ref + i + rr];
         out[op + i + (int)lane] = b;
       }
-    }  // off == 0: the reference copies the destination onto itself
+    } else {
+      // offset 0: the reference copies its destination onto itself, bytes it
+      // never wrote (new[] memory: undefined).  Here they are zeros, never the
+      // previous value decoded in this LDS window.
+#pragma unroll 1
+      for (int i = 0; i < mlen; i += 64) out[op + i + (int)lane] = 0;
+    }
     asm volatile("" ::: "memory");
     op += mlen;
   }
@@ -476,11 +485,14 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
                 o[opl + j] = b;
               }
             }
-          } else {
+          } else {                                // offset 0: zeros (see decode_block)
 #pragma unroll 1
             for (int i = 0; i < steps; i += 64) {
               const int j = i + (int)lane;
-              if (j < mlen) o[opl + j] = ring[(uint32_t)(opl + j) & kOMask];
+              if (j < mlen) {
+                ring[(uint32_t)(opl + j) & kOMask] = 0;
+                o[opl + j] = 0;
+              }
             }
           }
         } else {
@@ -614,11 +626,14 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
       }
     } else {
       // off == 0: the reference copies the destination onto itself (bytes it
-      // never wrote); the output is unspecified -- write the ring's bytes
+      // never wrote: undefined) -- zeros here, never an earlier value's bytes
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
         const int j = i + (int)lane;
-        if (j < mlen) o[op + j] = ring[(uint32_t)(op + j) & kOMask];
+        if (j < mlen) {
+          ring[(uint32_t)(op + j) & kOMask] = 0;
+          o[op + j] = 0;
+        }
       }
     }
     asm volatile("" ::: "memory");
@@ -750,7 +765,9 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t batch = claim_batch(n, grid);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
                      out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out));
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return work_counter_release(st, work);
 }
 
 template <bool F, uint32_t R>
@@ -767,19 +784,17 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
                      dst_off, out_cap, target, out_len, ret, work, batch, prio);
-  return hipGetLastError();
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return work_counter_release(st, work);
 }
 
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* e = getenv(name);
-  return e && *e ? (uint32_t)strtoul(e, nullptr, 0) : dflt;
-}
 
 template <bool F>
 static hipError_t launch_ring(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
                               uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst, const uint64_t* dst_off,
                               const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
-  static const uint32_t ring = env_u32("KDB_LZ4_ORING", 4096u);
+  static const uint32_t ring = (uint32_t)kdb_tune("KDB_LZ4_ORING", 4096);
   switch (ring) {
     case 8192u:
       return launch_big<F, 8192u>(st, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
@@ -809,7 +824,7 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   if (n == 0) return hipSuccess;
   // LDS-resident decoder up to `split` output bytes, the ring decoder above
-  static const uint32_t split = min(env_u32("KDB_LZ4_DSPLIT", 8192u), kOutSmallMax);
+  static const uint32_t split = min((uint32_t)kdb_tune("KDB_LZ4_DSPLIT", 8192), kOutSmallMax);
   const uint32_t in_split = split + split / 255u + 16u + 8u;
   const bool big = max_out > split || max_in > in_split;
   const uint32_t mi = max_in < in_split ? max_in : in_split;

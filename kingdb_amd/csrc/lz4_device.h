@@ -66,7 +66,7 @@ struct WorkQueue {
   uint32_t n, batch, cur, end, nr, q, left;
   // nr ranges: 1, or kQueues for launches whose claim rate would saturate one
   // counter (work_queues() on the host picks)
-  // c == nullptr: a direct launch (grid == n, see direct_grid), workgroup b
+  // c == nullptr: a direct launch (grid == n, see launch_counter), workgroup b
   // takes value b and nothing else -- no counter, so no memset before it.
   __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr) {
     if (!c) return WorkQueue{c, n, batch, blockIdx.x, min(blockIdx.x + 1u, n), 1u, 0u, 0u};
@@ -155,7 +155,16 @@ __device__ __forceinline__ void flush_lds_to_global(uint8_t* g, const uint8_t* l
   if (lane < n - done) g[done + lane] = lds_base[off + done + lane];
 }
 
+// Diagnostic knobs for A/B experiments (class splits, ring sizes, grid caps,
+// stream fork): read from the environment only in a build with
+// -DKDB_LZ4_TUNING (tools/build_variants.sh <name>:-DKDB_LZ4_TUNING); the
+// shipped library always uses the defaults.
+long kdb_tune(const char* name, long dflt);
+
 hipError_t work_counter(hipStream_t st, uint32_t** ctr);
+// after the launches reading a counter slot are queued on st: fences the slot
+// against reuse (launch_util.hip)
+hipError_t work_counter_release(hipStream_t st, uint32_t* ctr);
 uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
 // The launch's work counter: a direct launch (n no larger than the resident
 // grid, so one value per workgroup) needs none (*ctr = nullptr, no memset:

@@ -96,7 +96,8 @@ def read_hstable(f: bytes) -> list[Entry]:
     return out
 
 
-def get_values(items, verify: int = 0, stream: Stream | None = None) -> list[tuple[int, bytes]]:
+def get_values(items, verify: int = 0, stream: Stream | None = None,
+               frame_cap: int | None = None) -> list[tuple[int, bytes]]:
     """items: (stored bytes, size_value_compressed, size_value[, checksum, checksum_initial]).
     One GPU batch of CompressorLZ4::UncompressByteArray."""
     n = len(items)
@@ -119,9 +120,10 @@ def get_values(items, verify: int = 0, stream: Stream | None = None) -> list[tup
     obytes = int(ooff[-1] + size[-1]) + 64
     # frames are at least 8 bytes: Σ(avail/8 + 1) bounds them (values KingDB
     # writes hold one frame per part, far fewer)
-    frame_cap = int((avail // 8 + 1).sum())
-    if frame_cap > (4 << 20):
-        frame_cap = max(4 * n + int(avail.sum()) // 4096, 4 << 20)
+    if frame_cap is None:   # frames are >= 8 bytes: this many always suffice
+        frame_cap = int((avail // 8 + 1).sum())
+        if frame_cap > (4 << 20):
+            frame_cap = max(4 * n + int(avail.sum()) // 4096, 4 << 20)
     max_in = int(avail.max())
     max_out = int(size.max()) if n else 0
     sb = int(lib().kdb_get_scratch_bytes(n, frame_cap))
@@ -138,10 +140,12 @@ def get_values(items, verify: int = 0, stream: Stream | None = None) -> list[tup
         _lib.check(lib().kdb_get_values_batch(
             st, d_st.ptr, b, b + 8 * n, b + 16 * n, b + 24 * n, n, d_out.ptr, b + 32 * n, verify, b + 40 * n,
             b + 44 * n, frame_cap, max_in, max_out, d_scr.ptr, sb, p_outlen, p_status), "kdb_get_values_batch")
-        res = meta.download(12 * n, 48 * n)
+        # the copies back ride the same stream (a download on the null stream
+        # would not wait for a non-blocking caller stream)
+        res = meta.download(12 * n, 48 * n, stream=st)
         olen = res[: 8 * n].view(np.uint64)
         stat = res[8 * n:].view(np.int32)
-        out = d_out.download(obytes)
+        out = d_out.download(obytes, stream=st)
         return [(int(stat[i]), out[int(ooff[i]):int(ooff[i]) + int(olen[i])].tobytes()) for i in range(n)]
     finally:
         for d in (d_st, d_out, d_scr, meta):

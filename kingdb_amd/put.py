@@ -145,9 +145,10 @@ def put_entries(puts, hash_type: int = 1, stream: Stream | None = None) -> PutBa
             b.chunks.upload(clen, stream=st)
         b.run_device(stream, n, nparts, int(clen.max()) if nparts else 0, raw, hash_type)
         o = b._optr(n)
-        out = b.out.download(32 * n + 8, 0)
+        # the copies back ride the caller's stream (see get_values)
+        out = b.out.download(32 * n + 8, 0, stream=st)
         total = int(out[32 * n:32 * n + 8].view(np.uint64)[0])
-        ents = b.entries.download(total) if total else np.zeros(0, np.uint8)
+        ents = b.entries.download(total, stream=st) if total else np.zeros(0, np.uint8)
         del o
         return PutBatchResult(
             entries=ents, entry_off=out[0:8 * n].view(np.uint64).copy(), entry_len=out[8 * n:12 * n].view(np.uint32).copy(),

@@ -107,3 +107,95 @@ def test_gloo_world2_stitch(tmp_path, orc):
     assert bytes(stitched) == whole
     assert spans[0][0] == 0 and spans[0][1] == spans[1][0] and spans[1][1] == len(values)
     assert 0 < spans[0][1] < len(values)
+
+
+# ------------------------------------------------------------------ GPU
+def _gpu_worker(rank, world, port, out_dir):
+    """One rank per device (round-robin onto the visible GPUs, as bench.py maps
+    ranks): the rank's shard goes through the HIP codec."""
+    import torch.distributed as dist
+
+    import kingdb_amd as K
+    import oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    K.set_device(rank % K.device_count())
+    orc = oracle.Oracle()
+    pool = oracle.g1_pool(orc)
+    values = oracle.g1_values(pool, 100, 3000) + oracle.g1_values(pool, 4096, 300) + \
+        oracle.g1_values(pool, 65536, 8) + [bytes(5000), b"", bytes(range(256)) * 300]
+    lo, hi = byte_balanced_ranges([len(v) for v in values], world)[rank]
+    frames = K.compress_frames(values[lo:hi])
+    back = K.decompress_frames(frames, [len(v) for v in values[lo:hi]])
+    ok = all(st == 0 and out == v for (st, out), v in zip(back, values[lo:hi]))
+    mine = b"".join(frames)
+    totals = [None] * world
+    dist.all_gather_object(totals, len(mine))
+    off = int(stitch_offsets(totals)[rank])
+    with open(os.path.join(out_dir, f"rank{rank}.bin"), "wb") as f:
+        f.write(mine)
+    with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
+        f.write(f"{off} {int(ok)} {lo} {hi}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_world2_ranks_stitch_to_reference_stream(tmp_path, gpu, orc):
+    """world_size 2, each rank compressing (and round-tripping) its byte-balanced
+    shard on its own device: the stitched frame stream equals the oracle's
+    stream of the whole batch."""
+    import torch.multiprocessing as mp
+
+    import oracle
+    world = 2
+    mp.spawn(_gpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    pool = oracle.g1_pool(orc)
+    values = oracle.g1_values(pool, 100, 3000) + oracle.g1_values(pool, 4096, 300) + \
+        oracle.g1_values(pool, 65536, 8) + [bytes(5000), b"", bytes(range(256)) * 300]
+    whole = b"".join(orc.frame(v) for v in values)
+    stitched = bytearray(len(whole))
+    for r in range(world):
+        off, ok, lo, hi = (tmp_path / f"rank{r}.txt").read_text().split()
+        assert ok == "1", f"rank {r} round trip"
+        data = (tmp_path / f"rank{r}.bin").read_bytes()
+        stitched[int(off):int(off) + len(data)] = data
+    assert bytes(stitched) == whole
+
+
+@pytest.mark.gpu
+def test_gpu_host_threads_share_the_library(gpu, orc):
+    """INTEGRATION.md's in-process model: one host thread per device (here 4
+    threads round-robin on the visible devices), each with its own batches and
+    scalar calls at once -- per-thread streams, staging and fork streams."""
+    import threading
+
+    import kingdb_amd as K
+    import oracle
+    pool = oracle.g1_pool(orc)
+    errs = []
+
+    def work(t):
+        try:
+            K.set_device(t % K.device_count())
+            vals = oracle.g1_values(pool, 100 + 997 * t, 400) + [bytes(range(256)) * (t + 1)]
+            for _ in range(3):
+                fr = K.compress_frames(vals)
+                if fr != [orc.frame(v) for v in vals]:
+                    errs.append((t, "frames"))
+                back = K.decompress_frames(fr, [len(v) for v in vals])
+                if any(st != 0 or out != v for (st, out), v in zip(back, vals)):
+                    errs.append((t, "round trip"))
+                for v in vals[:20]:
+                    r, blk = K.compress_limited_output(v, K.compress_bound(len(v)))
+                    if blk != orc.compress(v):
+                        errs.append((t, "scalar"))
+        except Exception as e:  # noqa: BLE001
+            errs.append((t, repr(e)))
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert errs == []
