@@ -14,6 +14,14 @@ with the reference codec, run beside it as the checker.
     them LZ4): `==== PASSED` with the same test list as the reference build.
   * unit-tests/client_embedded.cc: 1 M puts of 16 B keys / 100 B values through
     Database::PutPart, then an iteration with GetValue: all 1 M items back.
+
+`oracle/_ref/kingdb_hook/` is the drop-in build plus the write-buffer flush
+hook (kingdb_amd/kingdb_include/cache/lz4_flush.h): single-part
+puts are queued raw and compressed, checksummed and sized at the flush in one
+kdb_put_entries_batch call.  The same test_db stages run against it, and the
+write-path driver oracle/ref_db.cc (built as kdb_db) must write the HSTable
+files the reference wrote for the golden put streams
+(tests/golden/hstable_streams.npz) byte for byte, through both builds.
 """
 import os
 import re
@@ -26,6 +34,8 @@ from conftest import ROOT, load_golden
 pytestmark = pytest.mark.gpu
 
 DROP = os.path.join(ROOT, "oracle", "_ref", "kingdb_dropin")
+HOOK = os.path.join(ROOT, "oracle", "_ref", "kingdb_hook")
+BUILDS = {"dropin": DROP, "hook": HOOK}
 REF = os.path.join(ROOT, "oracle", "_ref", "kingdb_ref")
 
 
@@ -71,12 +81,13 @@ QUICK = ["CloseAndReopen", "KeysWithNullBytes", "MultipartReader", "SingleThread
          "SingleThreadSnapshot", "SingleThreadSingleLargeEntry", "FileUtil"]
 
 
+@pytest.mark.parametrize("build", sorted(BUILDS))
 @pytest.mark.parametrize("name", [None] if os.environ.get("KDB_DROPIN_FULL") else QUICK)
-def test_kingdb_test_db(tmp_path, gpu, name):
+def test_kingdb_test_db(tmp_path, gpu, name, build):
     env = dict(os.environ)
     if name:
         env["LEVELDB_TESTS"] = name
-    r = subprocess.run([_bin(DROP, "test_db")], cwd=tmp_path, capture_output=True, text=True, env=env,
+    r = subprocess.run([_bin(BUILDS[build], "test_db")], cwd=tmp_path, capture_output=True, text=True, env=env,
                        timeout=1500, errors="replace")
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     tests, passed = _passed(r.stderr)
@@ -90,8 +101,33 @@ def test_kingdb_test_db(tmp_path, gpu, name):
 
 
 @pytest.mark.skipif(not os.environ.get("KDB_DROPIN_FULL"), reason="1 M puts; KDB_DROPIN_FULL=1")
-def test_kingdb_client_embedded(tmp_path, gpu):
-    r = subprocess.run([_bin(DROP, "client_emb")], cwd=tmp_path, capture_output=True, text=True, timeout=1500)
+@pytest.mark.parametrize("build", sorted(BUILDS))
+def test_kingdb_client_embedded(tmp_path, gpu, build):
+    r = subprocess.run([_bin(BUILDS[build], "client_emb")], cwd=tmp_path, capture_output=True, text=True,
+                       timeout=1500)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "count items: 1000000" in r.stdout
-    print(r.stdout)
+    print(build, r.stdout)
+
+
+def _golden_streams():
+    import numpy as np
+    z = np.load(os.path.join(ROOT, "tests", "golden", "hstable_streams.npz"))
+    return z, [str(n) for n in z["names"]]
+
+
+@pytest.mark.parametrize("build", sorted(BUILDS))
+@pytest.mark.parametrize("name", _golden_streams()[1])
+def test_kingdb_write_path_reference_hstables(tmp_path, gpu, build, name):
+    z, _ = _golden_streams()
+    hs, ht, mps = (int(x) for x in z[f"{name}__opts"])
+    (tmp_path / "s.bin").write_bytes(z[f"{name}__stream"].tobytes())
+    db = tmp_path / "db"
+    r = subprocess.run([_bin(BUILDS[build], "kdb_db"), str(db), str(tmp_path / "s.bin"), str(mps), str(hs), str(ht)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = [str(f) for f in z[f"{name}__files"]]
+    got = sorted(f for f in os.listdir(db) if len(f) == 8 and all(c in "0123456789abcdef" for c in f))
+    assert got == want
+    for f in want:
+        assert (db / f).read_bytes() == z[f"{name}__file_{f}"].tobytes(), f

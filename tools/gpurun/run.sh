@@ -17,6 +17,9 @@
 #   sq         SQ counter passes of the headline (tools/pmc.sh)
 #   dropin     KingDB's unit tests built against the drop-in (tests/test_kingdb_dropin.py)
 #   dropinfull the same with the whole test_db and client_emb (KDB_DROPIN_FULL=1)
+#   hook       the flush-hook build's tests only (test_kingdb_dropin.py -k hook)
+#   wpath      KingDB's write path (kdb_db) with the reference codec, the drop-in and
+#              the flush hook, 1 M x 100 B + 128 Ki x 4 KiB, on /tmp and on /dev/shm
 #   scalar     per-call latency of CompressorLZ4::Compress/Uncompress, drop-in vs reference
 #   ab:<NAME>=<VAL>  the quick headline line with one environment knob set
 #   var:<name> A/B of kingdb_amd/var/var_<name>.so (tools/ab.py, digest-gated)
@@ -76,6 +79,14 @@ for s in "$@"; do
       timeout -k 10 1100 python -u -m pytest tests/test_kingdb_dropin.py -x -v -s -m gpu --durations=0 --timeout 1000 --timeout-method thread > "${O}_$s.log" 2>&1 || fail $s $? "${O}_$s.log"
       grep -E "PASSED|FAILED|passed|failed|done in|count items|s call" "${O}_$s.log" | tail -30
       unset KDB_DROPIN_FULL ;;
+    hook)
+      timeout -k 10 900 python -u -m pytest tests/test_kingdb_dropin.py -x -v -s -m gpu -k hook --timeout 600 --timeout-method thread > "${O}_hook.log" 2>&1 || fail hook $? "${O}_hook.log"
+      grep -E "PASSED|FAILED|passed|failed" "${O}_hook.log" | tail -30 ;;
+    wpath)
+      for d in /tmp /dev/shm; do
+        timeout -k 10 900 python -u tools/write_path_cmp.py --dir $d --out "${O}_wpath_${d//\//_}.json" > "${O}_wpath.log" 2>&1 || fail wpath $? "${O}_wpath.log"
+        cat "${O}_wpath.log"
+      done ;;
     scalar)   # per-call latency of CompressorLZ4, drop-in (GPU) vs reference codec (CPU)
       for sz in 100 4096 65536; do
         for v in kingdb_ref kingdb_dropin; do

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""KingDB's own write path, like for like, with three codecs behind it.
+
+configs[4] (BASELINE.json): the sequential-write bench shape, 16 B keys /
+100 B values (and 4 KiB values beside it), sent through Database::PutPart ->
+WriteBuffer -> HSTableManager by oracle/ref_db.cc (built as kdb_db) in three
+builds of the SAME KingDB sources (oracle/Makefile):
+
+  kingdb_ref     the reference codec (algorithm/compressor.cc + lz4.cc) on the CPU
+  kingdb_dropin  the drop-in CompressorLZ4: one GPU call per PutPart (zero-copy
+                 scalar path, kdb_lz4_capi.hip)
+  kingdb_hook    the drop-in plus the flush hook (lz4_flush.h): one
+                 kdb_put_entries_batch per write-buffer flush
+
+Each build writes its HSTables into its own fresh directory under the SAME
+parent (--dir; default: the current directory, i.e. the box's local disk;
+/dev/shm for tmpfs), and the three databases' files must be identical.
+Prints one JSON object per (workload, build) and a summary line.
+
+  python tools/write_path_cmp.py [--n 1048576] [--sizes 100,4096] [--dir DIR]
+"""
+import argparse
+import json
+import os
+import shutil
+import struct
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+BUILDS = ["kingdb_ref", "kingdb_dropin", "kingdb_hook"]
+
+
+def stream(n: int, ks: int, vs: int) -> np.ndarray:
+    """n single-chunk puts, keys %016d-style, G1 values (oracle's generator)."""
+    import oracle  # the data generator only (checker infrastructure)
+    orc = oracle.Oracle()
+    pool = np.frombuffer(oracle.g1_pool(orc, 8 << 20), np.uint8)
+    rng = np.random.default_rng(7)
+    starts = rng.integers(0, len(pool) - vs, n)
+    vals = pool[starts[:, None] + np.arange(vs)[None, :]]
+    keys = np.frombuffer(b"".join(b"%016d" % i for i in range(n)), np.uint8).reshape(n, 16)[:, :ks]
+    rec = np.zeros((n, 4 + ks + 8 + 4 + 4 + vs), np.uint8)
+    rec[:, 0:4] = np.frombuffer(struct.pack("<I", ks), np.uint8)
+    rec[:, 4:4 + ks] = keys
+    rec[:, 4 + ks:12 + ks] = np.frombuffer(struct.pack("<Q", vs), np.uint8)
+    rec[:, 12 + ks:16 + ks] = np.frombuffer(struct.pack("<I", 1), np.uint8)
+    rec[:, 16 + ks:20 + ks] = np.frombuffer(struct.pack("<I", vs), np.uint8)
+    rec[:, 20 + ks:] = vals
+    return rec
+
+
+def files_of(db: str) -> dict:
+    return {f: open(os.path.join(db, f), "rb").read() for f in sorted(os.listdir(db))
+            if len(f) == 8 and all(c in "0123456789abcdef" for c in f)}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--sizes", default="100,4096")
+    ap.add_argument("--dir", default=".")
+    ap.add_argument("--builds", default=",".join(BUILDS))
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    rows = []
+    for vs in (int(x) for x in a.sizes.split(",")):
+        n = a.n if vs <= 1024 else max(1, a.n // 8)
+        d = tempfile.mkdtemp(prefix="kdbwp", dir=a.dir)
+        try:
+            sp = os.path.join(d, "s.bin")
+            stream(n, 16, vs).tofile(sp)
+            ref_files = None
+            for b in a.builds.split(","):
+                exe = os.path.join(ROOT, "oracle", "_ref", b, "kdb_db")
+                db = os.path.join(d, "db_" + b)
+                t0 = time.perf_counter()
+                r = subprocess.run([exe, db, sp], capture_output=True, text=True, timeout=900)
+                wall = time.perf_counter() - t0
+                if r.returncode != 0:
+                    print(r.stderr[-2000:], file=sys.stderr)
+                    sys.exit(f"{b} failed rc={r.returncode}")
+                f = r.stdout.split()
+                t_put, t_all = float(f[2]), float(f[5])
+                files = files_of(db)
+                if ref_files is None:
+                    ref_files = files
+                same = files == ref_files
+                row = {"workload": f"{n} puts 16 B keys / {vs} B G1 values", "build": b,
+                       "puts_per_s": round(n / t_put, 1), "puts_per_s_with_close": round(n / t_all, 1),
+                       "seconds_put": round(t_put, 4), "seconds_with_close": round(t_all, 4),
+                       "process_wall_s": round(wall, 3), "hstable_files": len(files),
+                       "hstable_bytes": sum(map(len, files.values())), "files_identical_to_first_build": same,
+                       "dir": os.path.abspath(a.dir)}
+                print(json.dumps(row), flush=True)
+                rows.append(row)
+                shutil.rmtree(db, ignore_errors=True)
+                if not same:
+                    sys.exit(f"{b}: HSTable files differ from {a.builds.split(',')[0]}")
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    if a.out:
+        json.dump(rows, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
