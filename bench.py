@@ -60,8 +60,9 @@ def parse():
     p.add_argument("--hi-chunk", type=int, default=1 << 16, help="values per pipeline chunk")
     p.add_argument("--hi-streams", type=int, default=4)
     p.add_argument("--put-chunk", type=int, default=1 << 17, help="put workload: puts per pipeline chunk")
-    p.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                   help="HBM traffic summary written by tools/pmc_traffic.py")
+    p.add_argument("--pmc", default=None,
+                   help="HBM traffic summary written by tools/pmc_traffic.py (default: "
+                        "profiles/pmc_traffic.json, profiles/pmc_traffic_mixed.json for --workload mixed)")
     return p.parse_args()
 
 
@@ -122,6 +123,78 @@ def cpu_baseline(sample: np.ndarray, size: int, seconds: float) -> dict:
                    "from the reference (oracle/_ref)" if kind == "reference" else
                    "oracle/lz4_oracle.c restatement (reference build absent)"),
     }
+
+
+def cpu_baseline_mixed(sample: np.ndarray, off: np.ndarray, lens: np.ndarray, seconds: float) -> dict | None:
+    """configs[3]'s CPU path: the reference's algorithm/lz4.cc round trip
+    (oracle/_ref ref_bench_roundtrip_var) over a bounded prefix of the same
+    mixed batch, every value one block as CompressorLZ4 makes it; None where the
+    reference build is absent."""
+    import oracle  # checker / baseline only
+    if not os.path.exists(oracle.REF_SO):
+        return None
+    lib = ctypes.CDLL(oracle.REF_SO)
+    fn = lib.ref_bench_roundtrip_var
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                   ctypes.POINTER(ctypes.c_uint64)]
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    off = np.ascontiguousarray(off, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+
+    def run(n, th, passes):
+        tc, td, cb = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        if fn(sample.ctypes.data, off.ctypes.data, lens.ctypes.data, n, th, passes, ctypes.byref(tc),
+              ctypes.byref(td), ctypes.byref(cb)) != 0:
+            raise RuntimeError("CPU baseline round trip failed")
+        return tc.value, td.value
+
+    res = {}
+    nall = len(lens)
+    for label, th, n, budget in (("all", threads, nall, 0.7 * seconds), ("one", 1, max(nall // 16, 1024), 0.3 * seconds)):
+        n = min(n, nall)
+        tc, td = run(n, th, 1)
+        passes = int(min(50, max(1, math.ceil(budget / max(tc + td, 1e-3)))))
+        tc, td = run(n, th, passes)
+        raw = float(lens[:n].astype(np.int64).sum()) * passes
+        res[label] = dict(rt=raw / (tc + td) / GIB, c=raw / tc / GIB, d=raw / td / GIB, n=n, passes=passes)
+    a, o = res["all"], res["one"]
+    return {
+        "value": round(a["rt"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+        "sample": (f"the first {a['n']} values of the mixed batch ({int(lens.astype(np.int64).sum())} B), "
+                   f"{a['passes']} timed round-trip passes after 1 warm-up, byte-balanced over {threads} threads; "
+                   f"CPU: {cpu_model()}"),
+        "compress_gibs": round(a["c"], 3), "decompress_gibs": round(a["d"], 3),
+        "one_thread": {"value": round(o["rt"], 3), "compress_gibs": round(o["c"], 3),
+                       "decompress_gibs": round(o["d"], 3), "values": o["n"], "passes": o["passes"]},
+        "source": "algorithm/lz4.cc LZ4_compress_limitedOutput + LZ4_decompress_safe_partial, compiled "
+                  "from the reference (oracle/_ref)",
+    }
+
+
+def compressor_calls_100b() -> dict | None:
+    """configs[0]: unit-tests/test_compression.cc's shape -- CompressorLZ4 on
+    100-byte values, one thread -- timed with the reference's own class
+    (oracle/_ref/kingdb_ref/bench_compressor, built from /root/reference) and
+    with the drop-in class (oracle/_ref/kingdb_dropin/bench_compressor: one GPU
+    call per value, the scalar zero-copy path); None where not built."""
+    import subprocess
+    out = {}
+    for kind, d in (("reference", "kingdb_ref"), ("dropin", "kingdb_dropin")):
+        exe = os.path.join(ROOT, "oracle", "_ref", d, "bench_compressor")
+        if not os.path.exists(exe):
+            return None
+        r = subprocess.run([exe, "100", "20000" if kind == "reference" else "2000"], capture_output=True, text=True,
+                           timeout=300)
+        if r.returncode != 0:
+            out[kind] = {"error": f"rc={r.returncode}: {r.stderr.strip()[-200:]}"}
+            continue
+        j = json.loads(r.stdout.strip().splitlines()[-1])
+        out[kind] = {"compress_us": j["compress_us"], "uncompress_us": j["uncompress_us"], "calls": j["calls"]}
+    out["unit"] = "us per CompressorLZ4::Compress / Uncompress call, one thread, 100 B G1 values"
+    return out
 
 
 def host_inclusive(batch, n: int, size: int, args) -> dict:
@@ -534,11 +607,18 @@ def main() -> None:
     else:
         dom_key, dom_name, dom_ms = "decompress", kd, d_ms
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM bytes of the same launch(es) from committed PMC passes of this exact
+    # workload (tools/pmc_traffic.py); traffic_source names the file and its passes
+    traffic, traffic_source = None, None
+    pmc = args.pmc or os.path.join(ROOT, "profiles",
+                                   "pmc_traffic_mixed.json" if args.workload == "mixed" else "pmc_traffic.json")
     try:
-        pm = json.load(open(args.pmc))
-        if args.workload == "uniform" and pm.get("values") == n and pm.get("size") == size:
+        pm = json.load(open(pmc))
+        want = (args.values, "mixed") if args.workload == "mixed" else (n, size)
+        if (pm.get("values"), pm.get("size")) == want and (world == 1 or args.workload == "uniform"):
             traffic = pm["kernels"][dom_key]["hbm_bytes_per_launch"]
+            traffic_source = {"file": os.path.relpath(pmc, ROOT), "passes": pm.get("passes"),
+                              "scope": pm.get("scope", "the kind's dominant launch")}
     except (OSError, ValueError, KeyError):
         pass
 
@@ -573,7 +653,7 @@ def main() -> None:
         "roofline": {
             "bound": "hbm", "kernel": dom_name,
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_source,
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(dom_ms, 4),
             "copy_gbs": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 5),
         },
@@ -589,6 +669,15 @@ def main() -> None:
         ncpu = min(n, 131072)
         sample = batch.src.download(ncpu * size)
         line["cpu_baseline"] = cpu_baseline(sample, size, args.cpu_seconds)
+        line["configs0_compressor_100b"] = compressor_calls_100b()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "mixed":
+        # a prefix of the same batch, about 512 MiB of raw bytes
+        lens = batch.sizes
+        m = int(np.searchsorted(np.cumsum(lens.astype(np.int64)), 512 << 20)) + 1
+        m = min(m, n)
+        nbytes = int(batch.src_off[m - 1]) + int(lens[m - 1])
+        sample = batch.src.download(nbytes)
+        line["cpu_baseline"] = cpu_baseline_mixed(sample, batch.src_off[:m], lens[:m], args.cpu_seconds)
     batch.free()
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -187,6 +187,68 @@ extern "C" int ref_bench_roundtrip(const char* src, int n, int size, int threads
   return bad ? -1 : 0;
 }
 
+// The same round trip over values of mixed sizes (bench.py --workload mixed):
+// value i is src[off[i] .. off[i] + len[i]), every value one LZ4 block as
+// CompressorLZ4::Compress makes it (a 64 KiB part is one block); the threads
+// take contiguous byte-balanced ranges.
+extern "C" int ref_bench_roundtrip_var(const char* src, const uint64_t* off, const uint32_t* len, int n,
+                                       int threads, int passes, double* t_compress, double* t_decompress,
+                                       uint64_t* comp_bytes) {
+  std::vector<uint64_t> boff(n + 1, 0), ooff(n + 1, 0);
+  for (int i = 0; i < n; i++) {
+    boff[i + 1] = boff[i] + (uint64_t)LZ4_compressBound((int)len[i]);
+    ooff[i + 1] = ooff[i] + len[i];
+  }
+  std::vector<char> blocks(boff[n]);
+  std::vector<int> blen(n);
+  std::vector<char> out(ooff[n]);
+  std::vector<int> cut(threads + 1, n);
+  cut[0] = 0;
+  for (int t = 1, i = 0; t < threads; t++) {
+    const uint64_t want = ooff[n] * (uint64_t)t / (uint64_t)threads;
+    while (i < n && ooff[i] < want) i++;
+    cut[t] = i;
+  }
+  int bad = 0;
+  auto run = [&](bool comp) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) {
+      th.emplace_back([&, t]() {
+        for (int i = cut[t]; i < cut[t + 1]; i++) {
+          const int sz = (int)len[i], bound = (int)(boff[i + 1] - boff[i]);
+          if (comp) {
+            blen[i] = LZ4_compress_limitedOutput(src + off[i], &blocks[boff[i]], sz, bound);
+          } else {
+            int r = LZ4_decompress_safe_partial(&blocks[boff[i]], &out[ooff[i]], blen[i], sz, sz);
+            if (r != sz) bad = 1;
+          }
+        }
+      });
+    }
+    for (auto& x : th) x.join();
+  };
+  run(true);
+  run(false);
+  double tc = 0, td = 0;
+  for (int p = 0; p < passes; p++) {
+    auto a = std::chrono::steady_clock::now();
+    run(true);
+    auto b = std::chrono::steady_clock::now();
+    run(false);
+    auto c = std::chrono::steady_clock::now();
+    tc += std::chrono::duration<double>(b - a).count();
+    td += std::chrono::duration<double>(c - b).count();
+  }
+  uint64_t cb = 0;
+  for (int i = 0; i < n; i++) cb += (uint64_t)blen[i];
+  *t_compress = tc;
+  *t_decompress = td;
+  *comp_bytes = cb;
+  for (int i = 0; i < n && !bad; i++)
+    if (memcmp(&out[ooff[i]], src + off[i], len[i]) != 0) bad = 1;
+  return bad ? -1 : 0;
+}
+
 // ByteArray's size/checksum setters are private to KingDB's own classes; the
 // shim reaches them through one of the befriended names (NetworkTask lives in
 // network/server.h, which is not part of this build), exactly as

@@ -4,7 +4,12 @@ of `bench.py --steps K --warmup 0 --no-cpu-baseline`, corrected as
 gfx950 reports half the bytes of wide streaming reads -> doubled; WRITE_SIZE
 taken as is.  rocprofv3's derived FETCH_SIZE / WRITE_SIZE are in KiB.
 
-    python tools/pmc_traffic.py <pass_fetch_dir> <pass_write_dir> <values> <size> [out.json]
+    python tools/pmc_traffic.py <pass_fetch_dir> <pass_write_dir> <values> <size|mixed> [out.json]
+
+size "mixed" (bench.py --workload mixed): a step launches one kernel per size
+class and kind; the step's traffic of a kind is the SUM over its kernels (each
+launched once per step), matching the roofline's "all compress launches of the
+step".  Otherwise the kind's dominant (largest) kernel.
 """
 import csv
 import glob
@@ -14,7 +19,7 @@ import sys
 from collections import defaultdict
 
 
-def per_kernel(root, counter):
+def per_kernel(root, counter, total=False):
     vals = defaultdict(list)
     names = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
@@ -33,20 +38,26 @@ def per_kernel(root, counter):
     out = {}
     for (key, short), v in vals.items():
         m = sum(v) / len(v)
-        if key not in out or m > out[key]:
+        if total:
+            out[key] = out.get(key, 0.0) + m
+            names[key] = (names[key] + " + " if key in names else "") + short
+        elif key not in out or m > out[key]:
             out[key] = m
             names[key] = short
     return out, names
 
 
 def main():
-    fdir, wdir, n, size = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    fdir, wdir, n = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    size = sys.argv[4] if sys.argv[4] == "mixed" else int(sys.argv[4])
+    mixed = size == "mixed"
     out = sys.argv[5] if len(sys.argv) > 5 else os.path.join(os.path.dirname(__file__), "..", "profiles",
-                                                             "pmc_traffic.json")
-    fetch, names = per_kernel(fdir, "FETCH_SIZE")
-    write, names2 = per_kernel(wdir, "WRITE_SIZE")
+                                                             "pmc_traffic_mixed.json" if mixed else "pmc_traffic.json")
+    fetch, names = per_kernel(fdir, "FETCH_SIZE", mixed)
+    write, names2 = per_kernel(wdir, "WRITE_SIZE", mixed)
     names.update(names2)
-    res = {"values": n, "size": size,
+    res = {"values": n, "size": size, "passes": [os.path.normpath(fdir), os.path.normpath(wdir)],
+           "scope": "sum of the kind's launches in one step" if mixed else "the kind's dominant launch",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; KiB x 1024; "
                      "FETCH_SIZE doubled (gfx950 half-count of wide reads, MI355X_MICROARCH.md HBM section)",
            "kernels": {}}
