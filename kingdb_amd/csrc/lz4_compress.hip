@@ -510,21 +510,16 @@ __device__ __forceinline__ T sload(const T* p, uint32_t i) {
 // kFrame = true : CompressorLZ4::Compress per value; the slot must hold
 //   8 + compress_bound(S) bytes; frame_len[v] = frame bytes, ret[v] = 0 or -1.
 //
+// The values of [min_len, in_cap] bytes, staged in LDS at `smem` (kSmall:
+// the fixed 16 KiB layout -- Table12, then the value; else Table16, then the
+// value), taken from the WorkQueue on `work`.
 template <bool kFrame, bool kSmall>
-__global__ __launch_bounds__(64) void lz4_compress_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+__device__ __forceinline__ void values_loop(
+    uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
-    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
-    uint32_t cls, uint32_t nq) {
-  if (census && census[cls] == 0) return;      // no value of this size class in the batch
-  // kSmall: a fixed LDS layout, so every LDS address is a constant offset (a
-  // dynamic allocation's base costs a v_add per address)
-  constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u : 16u;
-  __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
-  uint8_t* const smem = kSmall ? smem_s : smem_d;
+    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, uint32_t nq) {
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
   constexpr uint32_t kTabBytes = kSmall ? kTable12Bytes : kTableBytes;
@@ -626,6 +621,24 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   }
 }
 
+template <bool kFrame, bool kSmall>
+__global__ __launch_bounds__(64) void lz4_compress_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
+    const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
+    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
+    uint32_t cls, uint32_t nq) {
+  if (census && census[cls] == 0) return;      // no value of this size class in the batch
+  // kSmall: a fixed LDS layout, so every LDS address is a constant offset (a
+  // dynamic allocation's base costs a v_add per address)
+  constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u : 16u;
+  __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
+  values_loop<kFrame, kSmall>(kSmall ? smem_s : smem_d, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
+                              dst_cap, frame_len, ret, work, batch, nq);
+}
+
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
   // 16 KiB: 10 per CU
@@ -640,17 +653,11 @@ size_t compress_lds_bytes(uint32_t max_len) {
 // place from global memory (L2), the 16 KiB table lives in LDS; one wave per
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
 template <bool kFrame, bool kWide>
-__global__ __launch_bounds__(64) void lz4_compress_big_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+__device__ __forceinline__ void big_values(
+    uint32_t* const tab32, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
-    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    const uint32_t* __restrict__ census, uint32_t cls, uint32_t prio) {
-  if (census && census[cls] == 0) return;      // no value of this size class in the batch
-  // the big class is a mixed batch's critical path: its waves win issue
-  // arbitration over the small classes' waves that fill the GPU beside them
-  if (prio) __builtin_amdgcn_s_setprio(2);
-  __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   const uint32_t lane = lane_id();
   // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
   using Tab = typename std::conditional<kWide, Table32, Table16>::type;
@@ -722,6 +729,46 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   }
 }
 
+template <bool kFrame, bool kWide>
+__global__ __launch_bounds__(64) void lz4_compress_big_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    const uint32_t* __restrict__ census, uint32_t cls, uint32_t prio) {
+  if (census && census[cls] == 0) return;      // no value of this size class in the batch
+  // the big class is a mixed batch's critical path: its waves win issue
+  // arbitration over the small classes' waves that fill the GPU beside them
+  if (prio) __builtin_amdgcn_s_setprio(2);
+  __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
+  big_values<kFrame, kWide>(tab32, src, src_off, src_len, n, min_len, max_len, dst, dst_off, dst_cap, frame_len,
+                            ret, work, batch);
+}
+
+// A batch with values on both sides of 4 KiB .. 8 KiB (a mixed batch): ONE
+// persistent launch, in the 16 KiB the small class needs.  Each wave first
+// takes the in-place values (8 KiB .. 65 546 B: Table16 over the whole 16
+// KiB), which are the long ones, then -- when they are all claimed -- the
+// small values (<= 4 KiB, Table12 + staging).  Waves leave the in-place pass
+// one by one as its claims run out and go straight to small values, so the
+// small class fills the in-place tail instead of competing with its start
+// (two concurrent launches split the CUs from the start and left the
+// in-place values' last rounds alone on the GPU).
+template <bool kFrame>
+__global__ __launch_bounds__(64) void lz4_compress_mixed_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t big_min, uint32_t big_max,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work_big,
+    uint32_t batch_big, uint32_t* __restrict__ work_small, uint32_t batch_small, uint32_t nq) {
+  __shared__ __attribute__((aligned(16))) uint32_t smem32[(kTable12Bytes + kSmallMax) / 4u];
+  big_values<kFrame, false>(smem32, src, src_off, src_len, n, big_min, big_max, dst, dst_off, dst_cap, frame_len,
+                            ret, work_big, batch_big);
+  __syncthreads();
+  values_loop<kFrame, true>(reinterpret_cast<uint8_t*>(smem32), src, src_off, src_len, n, 0u, kSmallMax, dst,
+                            dst_off, dst_cap, frame_len, ret, work_small, batch_small, nq);
+}
+
 // Values per size class (len <= b0, <= b1, <= b2, above), so that a class
 // launch with nothing to do returns at once instead of scanning the batch.
 __global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n, uint32_t b0, uint32_t b1,
@@ -776,6 +823,24 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   return work_counter_release(st, work);
 }
 
+template <bool F>
+static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                               uint32_t n, uint32_t big_min, uint32_t big_max, uint8_t* dst, const uint64_t* dst_off,
+                               const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret) {
+  auto kern = lz4_compress_mixed_kernel<F>;
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
+  uint32_t *wb = nullptr, *ws = nullptr;
+  hipError_t e = launch_counter(st, n, grid, &wb);
+  if (e == hipSuccess) e = launch_counter(st, n, grid, &ws);
+  if (e != hipSuccess) return e;
+  const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, big_min, big_max, dst, dst_off,
+                     dst_cap, frame_len, ret, wb, bb, ws, bs, work_queues(kSmallMax));
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = work_counter_release(st, wb)) != hipSuccess) return e;
+  return work_counter_release(st, ws);
+}
+
 // One launch per size class that [min_len, max_len] (the launch's bounds on
 // its values' lengths; the batch API passes min_len 0) intersects: <= 4 KiB
 // (two-plane table, 16 KiB LDS), 4 KiB .. 8 KiB (LDS-staged), 8 KiB .. 65 546 B
@@ -809,14 +874,22 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   }
   // The in-place classes (8 KiB .. 65 546 B, and byU32) go first, on a
   // forked stream when smaller classes follow: their values take longest,
-  // and the small classes fill the GPU around their tail.
+  // and the small classes fill the GPU around their tail.  With both the
+  // small and the byU16 in-place class, one launch takes both
+  // (lz4_compress_mixed_kernel: in-place values first, then the small ones).
+  const bool combo = on[0] && on[2];
   hipStream_t aux = st;
-  const bool fork = (on[2] || on[3]) && (on[0] || on[1]);
+  const bool fork = combo ? on[3] : ((on[2] || on[3]) && (on[0] || on[1]));
   if (fork) {
     e = fork_begin(st, &aux);
     if (e != hipSuccess) return e;
   }
-  if (on[2]) {
+  if (combo) {
+    e = frame ? launch_mixed<true>(st, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len, ret)
+              : launch_mixed<false>(st, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len, ret);
+    if (e != hipSuccess) return e;
+  }
+  if (on[2] && !combo) {
     e = frame ? launch_big<true, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
                                         ret, census, 2)
               : launch_big<false, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
@@ -830,7 +903,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                                         frame_len, ret, census, 3);
     if (e != hipSuccess) return e;
   }
-  if (on[0]) {
+  if (on[0] && !combo) {
     const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
     e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
                                        frame_len, ret, census, 0)

@@ -257,14 +257,13 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
 //   (header u32 size_compressed_stored, u32 size_source); in_len[v] = bytes
 //   available there; ret[v] = 0 (OK) / -1 (IOError); out_len[v] = *size_dest.
 template <bool kFrame>
-__global__ __launch_bounds__(64) void lz4_decompress_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+__device__ __forceinline__ void small_decode_loop(
+    uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
     uint32_t skip_big, uint32_t nq) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   // [staged block + 16 zero bytes][output window + 64 bytes of slack for the
   // decoder's unmasked 64-byte steps]; the register window may read 256 bytes
@@ -336,6 +335,19 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     }
     __syncthreads();
   }
+}
+
+template <bool kFrame>
+__global__ __launch_bounds__(64) void lz4_decompress_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
+    const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    uint32_t skip_big, uint32_t nq) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  small_decode_loop<kFrame>(smem, src, src_off, in_len, n, in_cap, out_cap_max, dst, dst_off, out_cap, target,
+                            out_len, ret, work, batch, skip_big, nq);
 }
 
 // ---------------------------------------------------------------------------
@@ -644,15 +656,12 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
 
 // Values of this launch's class: out size > out_small or block > in_small.
 template <bool kFrame, uint32_t kORing>
-__global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+__device__ __forceinline__ void ring_decode_loop(
+    uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t prio) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  if (prio) __builtin_amdgcn_s_setprio(2);     // a mixed batch's critical path (see launch_compress)
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   const uint32_t lane = lane_id();
   uint8_t* ring = smem;
   uint8_t* iring = smem + kORing;
@@ -744,6 +753,43 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
   }
 }
 
+template <bool kFrame, uint32_t kORing>
+__global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
+    const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    uint32_t prio) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  if (prio) __builtin_amdgcn_s_setprio(2);     // a mixed batch's critical path (see launch_compress)
+  ring_decode_loop<kFrame, kORing>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                   out_len, ret, work, batch);
+}
+
+// A batch with values on both sides of the LDS decoder's limit (a mixed
+// batch): ONE persistent launch in the ring decoder's LDS.  Each wave first
+// takes the ring decoder's values (the long ones), then -- once they are all
+// claimed -- the LDS decoder's (outputs up to out_small, which the launch
+// sizes so the staged block and window fit the same LDS), so the small values
+// fill the tail of the long ones instead of splitting the CUs with them from
+// the start (lz4_compress_mixed_kernel does the same on the write side).
+template <bool kFrame>
+__global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
+    const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work_big, uint32_t batch_big,
+    uint32_t* __restrict__ work_small, uint32_t batch_small, uint32_t nq) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  ring_decode_loop<kFrame, 4096u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                  out_len, ret, work_big, batch_big);
+  __syncthreads();
+  small_decode_loop<kFrame>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                            out_len, ret, work_small, batch_small, 1u, nq);
+}
+
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
   // staged block (16 B alignment head + block + 16 zero bytes) | output window
   // + 64 B slack; the register window reaches 256 B past the block
@@ -814,9 +860,32 @@ static hipError_t launch_ring(hipStream_t st, const uint8_t* src, const uint64_t
   }
 }
 
+template <bool F>
+static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
+                               uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst,
+                               const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
+                               uint32_t* out_len, int32_t* ret) {
+  auto kern = lz4_decompress_mixed_kernel<F>;
+  const size_t lds = ring_lds<4096u>();
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  uint32_t *wb = nullptr, *ws = nullptr;
+  hipError_t e = launch_counter(st, n, grid, &wb);
+  if (e == hipSuccess) e = launch_counter(st, n, grid, &ws);
+  if (e != hipSuccess) return e;
+  const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst, dst_off,
+                     out_cap, target, out_len, ret, wb, bb, ws, bs, work_queues(out_small));
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = work_counter_release(st, wb)) != hipSuccess) return e;
+  return work_counter_release(st, ws);
+}
+
 // LDS-resident decoder for outputs up to 65 546 bytes (blocks up to the bound
 // of that, plus a frame header); the ring decoder after it for the rest.
 constexpr uint32_t kOutSmallMax = k64KLimit - 1u;
+// the LDS decoder's limit inside lz4_decompress_mixed_kernel: its staged block
+// and window (decompress_lds_bytes) fit the ring decoder's LDS
+constexpr uint32_t kMixedOutSmall = 6144u;
 
 hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
@@ -836,6 +905,17 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
   hipError_t e = hipSuccess;
   // one block that the ring decoder owns (a scalar call): that launch alone
   const bool ring_only = !frame && n == 1u && big;
+  // both classes: one launch (lz4_decompress_mixed_kernel), the LDS decoder's
+  // limit lowered so that its staging fits the ring decoder's LDS
+  static const bool combo_on = kdb_tune("KDB_LZ4_DMIXED", 1) != 0;
+  if (big && !ring_only && combo_on) {
+    const uint32_t mo2 = min(mo, kMixedOutSmall);
+    const uint32_t mi2 = min(mi, kMixedOutSmall + kMixedOutSmall / 255u + 16u + 8u);
+    return frame ? launch_mixed<true>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target, out_len,
+                                      ret)
+                 : launch_mixed<false>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target, out_len,
+                                       ret);
+  }
   if (big) {
     if (!ring_only && (e = fork_begin(st, &aux)) != hipSuccess) return e;
     e = frame ? launch_ring<true>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)

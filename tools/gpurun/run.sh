@@ -14,6 +14,7 @@
 #   profmixed profput profget   the same for the other workloads
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the headline -> pmc_traffic.json
 #   pmcmixed   the same for the mixed batch
+#   pmcu:<size>:<values>  the same for a uniform batch of other sizes
 #   sq         SQ counter passes of the headline (tools/pmc.sh)
 #   dropin     KingDB's unit tests built against the drop-in (tests/test_kingdb_dropin.py)
 #   dropinfull the same with the whole test_db and client_emb (KDB_DROPIN_FULL=1)
@@ -71,6 +72,9 @@ for s in "$@"; do
     profget) prof get --workload get --no-cpu-baseline --steps 3 --warmup 1 ;;
     pmc) pmc bench 1048576 4096 ;;
     pmcmixed) pmc mixed 1048576 mixed --workload mixed ;;
+    pmcu:*)   # pmcu:<size>:<values> -- FETCH/WRITE passes of a uniform batch
+      a=${s#pmcu:}; sz=${a%%:*}; nv=${a#*:}
+      pmc u${sz} $nv $sz --size $sz --values $nv ;;
     sq)
       timeout -k 10 900 bash tools/pmc.sh "${O}_sq" python3 "$R/bench.py" --no-cpu-baseline --no-verify --steps 1 --warmup 0 || exit 1
       python tools/pmc_summary.py "${O}_sq" > "${O}_sq.txt" && cat "${O}_sq.txt" ;;

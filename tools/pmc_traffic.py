@@ -28,7 +28,7 @@ def per_kernel(root, counter, total=False):
                 continue
             full = row.get("Kernel_Name", "?")
             short = full.split("(")[0].replace("void ", "")
-            key = ("decompress" if "decompress_kernel" in short else "compress" if "compress_kernel" in short
+            key = ("decompress" if "lz4_decompress" in short else "compress" if "lz4_compress" in short
                    else "pack_copy" if "pack_copy" in short else "pack_scan" if "pack_scan" in short else None)
             if key is None:
                 continue
