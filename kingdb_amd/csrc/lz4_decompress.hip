@@ -105,23 +105,34 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // far_ip, op <= far_op make the not-last and output checks of any fast
       // sequence true (lit <= 60, mlen <= 273) -- and the rest are sign bits
       // of plain integer expressions.
+      //
+      // The next sequence's literal load goes out as soon as its token is
+      // known (v_readlane of this one's load), before this sequence's match
+      // copy, so the two LDS round trips of a sequence overlap.
       int vip = vgpr(ip), vop = vgpr(op);
       uint32_t vq = vgpr(q);
+      // a sequence's literal-run header from its token word tq at tip: lx (a
+      // literal-length byte follows), xl (its value or 0), lit, ls (first literal)
+      int lx, xl, lit, ls;
+      auto header = [&](uint32_t tq, int tip) {
+        const int ln = (int)(tq & 0xffu) >> 4, b1 = (int)((tq >> 8) & 0xffu);
+        lx = (ln + 1) >> 4;
+        xl = b1 & -lx;
+        lit = ln + xl;                                            // <= 60 iff !lx || b1 <= 45
+        ls = tip + 1 + lx;
+      };
+      header(vq, vip);
+      // lane i holds the block's 4 bytes from ls + i: byte 0 is literal i,
+      // and one readlane gives the offset + match-length byte, another the
+      // next token and the byte after it.  The load goes out before the
+      // fast-path test (its address is inside the staged block plus the
+      // window slack for any token; a sequence that fails the test never
+      // uses it), so both tests are one scalar decision.
+      uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
 #pragma unroll 1
       for (;;) {
-        const int tk = (int)(vq & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((vq >> 8) & 0xffu);
-        const int lx = (ln + 1) >> 4;                             // a literal-length byte follows
-        const int xl = b1 & -lx;                                  // its value, or 0
-        const int lit = ln + xl;                                  // <= 60 iff !lx || b1 <= 45
-        const int ls = vip + 1 + lx;
+        const int mn = (int)(vq & 0xffu) & (int)kMlMask;
         const int opl = vop + lit;
-        // lane i holds the block's 4 bytes from ls + i: byte 0 is literal i,
-        // and one readlane gives the offset + match-length byte, another the
-        // next token and the byte after it.  The load goes out before the
-        // fast-path test (its address is inside the staged block plus the
-        // window slack for any token; a sequence that fails the test never
-        // uses it), so both tests are one scalar decision.
-        const uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
         const uint32_t w = readlane(v, (uint32_t)unii(lit) & 63u);   // offset, match-length byte
         const int e = (int)((w >> 16) & 0xffu);
         const int off = (int)(w & 0xffffu);
@@ -134,6 +145,8 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         const int nt = lit + 2 + mx;                              // next token's lane (<= 63)
         vq = vgpr(readlane(v, (uint32_t)unii(nt)));
         vip = ls + nt;
+        header(vq, vip);
+        v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));   // the next sequence's literals
         const int ref = opl - off;
         asm volatile("" ::: "memory");
         if (unii(off - min(mlen, 64)) < 0) {
@@ -457,15 +470,22 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
       int vip = vgpr(ip), vop = vgpr(op);
       uint32_t vq = vgpr(q);
       int qok = 1;
+      // as in decode_block: the next sequence's literal load goes out before
+      // this sequence's match copy
+      int lx, xl, lit, ls;
+      auto header = [&](uint32_t tq, int tip) {
+        const int ln = (int)(tq & 0xffu) >> 4, b1 = (int)((tq >> 8) & 0xffu);
+        lx = (ln + 1) >> 4;
+        xl = b1 & -lx;
+        lit = ln + xl;
+        ls = tip + 1 + lx;
+      };
+      header(vq, vip);
+      uint32_t v = in.lds[((uint32_t)ls & kIMask) + lane];
 #pragma unroll 1
       for (;;) {
-        const int tk = (int)(vq & 0xffu), ln = tk >> 4, mn = tk & (int)kMlMask, b1 = (int)((vq >> 8) & 0xffu);
-        const int lx = (ln + 1) >> 4;
-        const int xl = b1 & -lx;
-        const int lit = ln + xl;
-        const int ls = vip + 1 + lx;
+        const int mn = (int)(vq & 0xffu) & (int)kMlMask;
         const int opl = vop + lit;
-        const uint32_t v = in.lds[((uint32_t)ls & kIMask) + lane];
         const uint32_t l3 = (uint32_t)unii(lit) & 63u;
         const int e = (int)readlane(v, (l3 + 2u) & 63u);
         const int off = (int)(readlane(v, l3) | (readlane(v, (l3 + 1u) & 63u) << 8));
@@ -481,6 +501,8 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
         const uint32_t nt = (uint32_t)unii(lit + 2 + mx);
         vq = vgpr(readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8));
         vip = ls + lit + 2 + mx;
+        header(vq, vip);
+        v = in.lds[((uint32_t)ls & kIMask) + lane];   // the next sequence's literals (in the ring + mirror)
         const int ref = opl - off;
         asm volatile("" ::: "memory");
         const int steps = unii(mlen);
