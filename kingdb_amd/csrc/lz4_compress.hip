@@ -495,16 +495,6 @@ __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint
   for (uint32_t c = lane_id(); c < chunks; c += 64u) l[c] = head ? funnel16(base[c], base[c + 1u], head) : base[c];
 }
 
-// Per-value metadata read through the scalar cache (s_load, counted by
-// lgkmcnt): a vector load would be counted by vmcnt behind the next value's
-// prefetch loads and the previous value's byte stores, and waiting for it
-// (vmcnt(0): the counts are not static) exposed the whole prefetch latency
-// at every value.
-template <class T>
-__device__ __forceinline__ T sload(const T* p, uint32_t i) {
-  return ((const __attribute__((address_space(4))) T*)p)[i];
-}
-
 // kFrame = false: LZ4_compress_limitedOutput per value; ret[v] = size or 0,
 //   dst slot capacity = cap[v].
 // kFrame = true : CompressorLZ4::Compress per value; the slot must hold

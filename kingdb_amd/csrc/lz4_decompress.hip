@@ -269,6 +269,34 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
 // kFrame = true : one CompressorLZ4 frame per value at src + src_off[v]
 //   (header u32 size_compressed_stored, u32 size_source); in_len[v] = bytes
 //   available there; ret[v] = 0 (OK) / -1 (IOError); out_len[v] = *size_dest.
+// Register prefetch: while a value is decoded, the next value's bytes (frame
+// header included) are already on their way from HBM as whole aligned
+// 16-byte chunks, so a value's start does not wait for two HBM round trips
+// (header, then block).  Values whose bytes do not fit kDPrefetch chunks per
+// lane (or the staging area) get chunks = 0 and are staged as before.
+constexpr uint32_t kDPrefetch = 5;
+__device__ __forceinline__ void prefetch_value(uint4& p0, uint4& p1, uint4& p2, uint4& p3, uint4& p4, uint32_t& head, uint32_t& chunks, uint32_t w,
+                                               uint32_t n, const uint8_t* __restrict__ src,
+                                               const uint64_t* __restrict__ src_off,
+                                               const uint32_t* __restrict__ in_len, uint32_t s_in_cap) {
+  chunks = 0;
+  if (w >= n) return;
+  const uint8_t* gp = src + sload(src_off, w);
+  const uint32_t len = sload(in_len, w);
+  const uint32_t hd = uni((uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u));
+  const uint32_t ch = (hd + len + 15u) >> 4;
+  if (len == 0 || hd + len + 16u > s_in_cap || ch > 64u * kDPrefetch) return;
+  head = hd;
+  chunks = ch;
+  const uint4* base = reinterpret_cast<const uint4*>(__builtin_assume_aligned(gp - hd, 16));
+  const uint32_t lane = lane_id();
+  p0 = base[min(lane, ch - 1u)];
+  p1 = base[min(lane + 64u, ch - 1u)];
+  p2 = base[min(lane + 128u, ch - 1u)];
+  p3 = base[min(lane + 192u, ch - 1u)];
+  p4 = base[min(lane + 256u, ch - 1u)];
+}
+
 template <bool kFrame>
 __device__ __forceinline__ void small_decode_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -282,71 +310,99 @@ __device__ __forceinline__ void small_decode_loop(
   // decoder's unmasked 64-byte steps]; the register window may read 256 bytes
   // past the block, into the output window (decompress_lds_bytes)
   uint8_t* s_in = smem;
-  uint8_t* s_out = smem + (((size_t)in_cap + 32u + 15u) & ~(size_t)15u);
+  const uint32_t s_in_cap = (in_cap + 32u + 15u) & ~15u;
+  uint8_t* s_out = smem + s_in_cap;
+
+  // the next value's bytes in flight in registers (prefetch_value)
+  uint4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {}, pf4 = {};
+  uint32_t pf_head = 0, pf_chunks = 0;
 
   WorkQueue wq = WorkQueue::make(work, n, batch, nq);
+  uint32_t v = uni(wq.next());
+  prefetch_value(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, v, n, src, src_off, in_len, s_in_cap);
 #pragma unroll 1
-  for (uint32_t v = wq.next(); v < n; v = wq.next()) {
-    const uint8_t* g = src + src_off[v];
-    uint8_t* o = dst + dst_off[v];
-    int csize, osize, tgt;
-    if (kFrame) {
-      // compressor.cc:89-90 (GetFixed32 x2)
-      const uint32_t stored =
-          uni((uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[2] << 16) | ((uint32_t)g[3] << 24));
-      const uint32_t raw =
-          uni((uint32_t)g[4] | ((uint32_t)g[5] << 8) | ((uint32_t)g[6] << 16) | ((uint32_t)g[7] << 24));
-      const uint32_t avail = uni(in_len[v]);
-      if (raw > uni(out_cap[v])) {
-        if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
-        continue;
-      }
-      if (stored == 0) {  // raw frame (compressor.cc:116-124)
-        if (raw + 8u > avail) {
-          if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
-          continue;
-        }
-        for (uint32_t i = lane; i < raw; i += 64u) o[i] = g[8u + i];
-        if (lane == 0) { ret[v] = 0; out_len[v] = raw; }
-        continue;
-      }
-      csize = (int)(stored - 8u);          // compressor.cc:96 (u32 wrap kept: int cast)
-      osize = (int)raw;
-      tgt = osize;                         // compressor.cc:103-107: target = max = size_source
-      g += 8;
-      if (csize < 0 || (uint32_t)csize + 8u > avail) {
-        // a negative size makes the reference return -2/-3 (IOError); a size past
-        // the bytes supplied would have it read foreign memory: IOError as well.
-        if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
-        continue;
-      }
-    } else {
-      csize = (int)uni(in_len[v]);
-      osize = (int)uni(out_cap[v]);
-      tgt = target ? (int)uni(target[v]) : osize;
+  while (v < n) {
+    const uint32_t vn = uni(wq.next());   // the next value, one ahead
+    // the prefetched bytes land in LDS (byte i of the value at s_in[head + i])
+    // before the registers take the next value's
+    const uint32_t st_head = pf_head, st_chunks = pf_chunks;
+    {
+      uint4* l4 = reinterpret_cast<uint4*>(s_in);
+      static_assert(kDPrefetch == 5, "landing below is written out for 5 chunks per lane");
+      if (lane < st_chunks) l4[lane] = pf0;
+      if (lane + 64u < st_chunks) l4[lane + 64u] = pf1;
+      if (lane + 128u < st_chunks) l4[lane + 128u] = pf2;
+      if (lane + 192u < st_chunks) l4[lane + 192u] = pf3;
+      if (lane + 256u < st_chunks) l4[lane + 256u] = pf4;
     }
-    if ((uint32_t)csize > in_cap || (uint32_t)osize > out_cap_max || csize < 0 || osize < 0) {
-      // values too large for this launch's LDS: the ring decoder's (its own
-      // launch, beside this one) when skip_big, else unsupported
-      if (skip_big && csize >= 0 && osize >= 0) continue;
-      if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
-      continue;
-    }
-    const uint32_t head = stage_to_lds(g, (uint32_t)csize, s_in);
-    if (lane < 16u) s_in[head + (uint32_t)csize + lane] = 0;   // OOB bytes read as 0
-    __syncthreads();
-    const int r = decode_block(s_in, head, csize, s_out, osize, tgt);
-    if (r > 0) flush_lds_to_global(o, s_out, 0, (uint32_t)r);
-    if (lane == 0) {
+    prefetch_value(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, vn, n, src, src_off, in_len, s_in_cap);
+    do {
+      const uint8_t* g = src + sload(src_off, v);
+      uint8_t* o = dst + sload(dst_off, v);
+      int csize, osize, tgt;
       if (kFrame) {
-        ret[v] = r > 0 ? 0 : -1;           // compressor.cc:109-115
-        out_len[v] = r > 0 ? (uint32_t)r : 0u;
+        // compressor.cc:89-90 (GetFixed32 x2)
+        uint32_t stored, raw;
+        if (st_chunks) {
+          stored = uni(lds_rd32(s_in, st_head));
+          raw = uni(lds_rd32(s_in, st_head + 4u));
+        } else {
+          stored = uni((uint32_t)g[0] | ((uint32_t)g[1] << 8) | ((uint32_t)g[2] << 16) | ((uint32_t)g[3] << 24));
+          raw = uni((uint32_t)g[4] | ((uint32_t)g[5] << 8) | ((uint32_t)g[6] << 16) | ((uint32_t)g[7] << 24));
+        }
+        const uint32_t avail = sload(in_len, v);
+        if (raw > sload(out_cap, v)) {
+          if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+          break;
+        }
+        if (stored == 0) {  // raw frame (compressor.cc:116-124)
+          if (raw + 8u > avail) {
+            if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+            break;
+          }
+          for (uint32_t i = lane; i < raw; i += 64u) o[i] = g[8u + i];
+          if (lane == 0) { ret[v] = 0; out_len[v] = raw; }
+          break;
+        }
+        csize = (int)(stored - 8u);          // compressor.cc:96 (u32 wrap kept: int cast)
+        osize = (int)raw;
+        tgt = osize;                         // compressor.cc:103-107: target = max = size_source
+        g += 8;
+        if (csize < 0 || (uint32_t)csize + 8u > avail) {
+          // a negative size makes the reference return -2/-3 (IOError); a size past
+          // the bytes supplied would have it read foreign memory: IOError as well.
+          if (lane == 0) { ret[v] = -1; out_len[v] = 0; }
+          break;
+        }
       } else {
-        ret[v] = r;
-        if (out_len) out_len[v] = r > 0 ? (uint32_t)r : 0u;
+        csize = (int)sload(in_len, v);
+        osize = (int)sload(out_cap, v);
+        tgt = target ? (int)sload(target, v) : osize;
       }
-    }
+      if ((uint32_t)csize > in_cap || (uint32_t)osize > out_cap_max || csize < 0 || osize < 0) {
+        // values too large for this launch's LDS: the ring decoder's (its own
+        // launch, beside this one) when skip_big, else unsupported
+        if (skip_big && csize >= 0 && osize >= 0) break;
+        if (lane == 0) { ret[v] = kUnsupported; if (out_len) out_len[v] = 0; }
+        break;
+      }
+      const uint32_t head = st_chunks ? st_head + (kFrame ? 8u : 0u) : stage_to_lds(g, (uint32_t)csize, s_in);
+      if (lane < 16u) s_in[head + (uint32_t)csize + lane] = 0;   // OOB bytes read as 0
+      __syncthreads();
+      const int r = decode_block(s_in, head, csize, s_out, osize, tgt);
+      if (r > 0) flush_lds_to_global(o, s_out, 0, (uint32_t)r);
+      if (lane == 0) {
+        if (kFrame) {
+          ret[v] = r > 0 ? 0 : -1;           // compressor.cc:109-115
+          out_len[v] = r > 0 ? (uint32_t)r : 0u;
+        } else {
+          ret[v] = r;
+          if (out_len) out_len[v] = r > 0 ? (uint32_t)r : 0u;
+        }
+      }
+    } while (false);
     __syncthreads();
+    v = vn;
   }
 }
 

@@ -101,6 +101,16 @@ struct WorkQueue {
   }
 };
 
+// Per-value metadata read through the scalar cache (s_load, counted by
+// lgkmcnt): a vector load would be counted by vmcnt behind the next value's
+// prefetch loads and the previous value's byte stores, and waiting for it
+// (vmcnt(0): the counts are not static) exposed the whole prefetch latency
+// at every value.
+template <class T>
+__device__ __forceinline__ T sload(const T* p, uint32_t i) {
+  return ((const __attribute__((address_space(4))) T*)p)[i];
+}
+
 // LZ4_compressBound (lz4.h:103).
 __host__ __device__ __forceinline__ uint32_t compress_bound(uint32_t n) {
   return n > kMaxInput ? 0u : n + n / 255u + 16u;
