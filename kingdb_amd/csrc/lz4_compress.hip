@@ -304,29 +304,23 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
       // mflimit without a match goes to the last literals)
-      uint32_t kb = 0, pk, refk, h;
+      uint32_t pk, refk, h;
       uint64_t mm, vm;
-      bool lead;
-#pragma unroll 1
-      for (;;) {
-        // positions: step(k) = 1 for k <= 64, so the first chunk is s-o3+lane
-        lead = kb == 0 && t0 != 0;
-        const uint32_t o3 = 3u * t0;
-        const uint32_t k = kb + lane - o3;
-        // kb is uniform: the first chunk's positions are consecutive (step 1),
-        // later chunks' k >= 61 take the closed form with no k == 0 case
+      // the lead chunk's lane masks, per sequence (t0 != 0: lane 0 put only,
+      // lane 1 dead, lane 2 valid unconditionally -- see above)
+      const uint64_t lead_or = t0 ? 5ull : 0ull, lead_and = t0 ? ~2ull : ~0ull;
+      const uint64_t lead_mm = t0 ? ~1ull : ~0ull, lead_full = t0 ? 2ull : 0ull;
+      const uint32_t o3 = 3u * t0;
+      uint32_t next_lane = t0 ? 2u : 64u;             // a match on this lane is _next_match
+      // First chunk (nearly every sequence's only one): step(k) = 1 for k <= 64,
+      // so its positions are s-o3+lane.
+      {
         pk = s - o3 + lane;
-        uint32_t nx = pk + 1u;
-        if (kb != 0) {
-          pk = search_pos_nz<kWide>(s, k);
-          nx = pk + ((63u + k) >> 6);
-        }
         // valid lanes (lz4.cc:510), as a compare straight into a lane mask
-        vm = __builtin_amdgcn_uicmp(nx, mflimit, 37 /*ULE*/);
-        if (lead) vm = (vm | 5ull) & ~2ull;
+        vm = (__builtin_amdgcn_uicmp(pk + 1u, mflimit, 37 /*ULE*/) | lead_or) & lead_and;
         const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
         const uint32_t seq = RD32(min(pk, last4));
-        if (!kGuard && kb == 0 && pe_total) {        // the pending sequence (first chunk only)
+        if (!kGuard && pe_total) {                   // the pending sequence
           const uint32_t j = lane;
           const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
           const uint32_t hb = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
@@ -345,11 +339,28 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // compare straight into a lane mask (a ballot of a bool would be
         // materialised in a VGPR and compared again); byU32 adds the
         // distance check (lz4.cc:526, 614), byU16 sizes never need it
-        mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm & (lead ? ~1ull : ~0ull);
+        mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm & lead_mm;
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
-        // one exit: a match, or the chunk ran past mflimit (last literals)
-        if (mm || (vm | (lead ? 2ull : 0ull)) != ~0ull) break;
-        kb += 64u;
+      }
+      // later chunks: no match yet and every lane valid (else: last literals)
+      if ((mm | ~(vm | lead_full)) == 0) {
+        uint32_t kb = 0;
+        next_lane = 64u;
+#pragma unroll 1
+        for (;;) {
+          kb += 64u;
+          // k >= 61: the closed form with no k == 0 case
+          const uint32_t k = kb + lane - o3;
+          pk = search_pos_nz<kWide>(s, k);
+          vm = __builtin_amdgcn_uicmp(pk + ((63u + k) >> 6), mflimit, 37 /*ULE*/);
+          const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);
+          const uint32_t seq = RD32(min(pk, last4));
+          h = hashp<kWide>(seq);
+          refk = tab.xchg(h, pk, valid);
+          mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm;
+          if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
+          if ((mm | ~vm) != 0) break;                // a match, or past mflimit
+        }
       }
       if (!mm) break;
       const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
@@ -360,7 +371,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // -- its refk is a position <= ip (positions grow with the lane; entries
       // from before the chunk are smaller still)
       if (__builtin_amdgcn_inverse_ballot_w64(vm) && lane > ks && refk <= ip) tab.restore(h, refk);
-      const bool catchup = !(lead && ks == 2u);   // a lane-2 match is _next_match
+      const bool catchup = ks != next_lane;       // a lane-2 match of a lead chunk is _next_match
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml;
