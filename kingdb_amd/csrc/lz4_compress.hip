@@ -263,6 +263,24 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
+// Byte j of a pending sequence's encoding (see emit_seq): token at 0, the
+// literal-length run's last byte at a-1, literals [a, b) (lb: this lane's
+// literal byte), offset at b, b+1, the match-length run's last byte at
+// total-1, 255 elsewhere.  Later overrides win where positions coincide (a
+// missing run's "last byte" falls on the token, resp. the offset's high
+// byte); one compare-select each, no branches.
+__device__ __forceinline__ uint32_t pending_byte(uint32_t j, uint32_t lb, uint32_t a, uint32_t b, uint32_t total,
+                                                 uint32_t tok, uint32_t remL, uint32_t remM, uint32_t off) {
+  uint32_t val = 255u;
+  val = j + 1u == a ? remL : val;
+  val = j + 1u == total ? remM : val;
+  val = j == b ? (off & 255u) : val;
+  val = j == b + 1u ? (off >> 8) : val;
+  val = j == 0u ? tok : val;
+  val = (j >= a && j < b) ? lb : val;
+  return val;
+}
+
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
@@ -277,7 +295,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
   // chunk: its literal read shares that chunk's first LDS round trip and its
   // selects and store fill the wait (unguarded mode only).
   int pe_pos = 0, pe_lbase = 0;
-  uint32_t pe_a = 0, pe_b = 0, pe_total = 0, pe_w0 = 0, pe_w1 = 0;   // w0 = tok|remL<<8|remM<<16, w1 = off
+  uint32_t pe_a = 0, pe_b = 0, pe_total = 0, pe_tok = 0, pe_remL = 0, pe_remM = 0, pe_off = 0;
 #define RD32(p) src.rd32(p)
 
   if (S >= kMinLength) {                                    // lz4.cc:483
@@ -323,11 +341,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         if (!kGuard && pe_total) {                   // the pending sequence
           const uint32_t j = lane;
           const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
-          const uint32_t hb = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
-          const uint32_t t = j == pe_b ? (pe_w1 & 255u)
-                           : j == pe_b + 1u ? (pe_w1 >> 8)
-                           : (j + 1u == pe_total ? (pe_w0 >> 16) : 255u);
-          const uint32_t val = j < pe_a ? hb : (j < pe_b ? lb : t);
+          const uint32_t val = pending_byte(j, lb, pe_a, pe_b, pe_total, pe_tok, pe_remL, pe_remM, pe_off);
           if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
           pe_total = 0;
         }
@@ -452,8 +466,10 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         pe_a = ea;
         pe_b = ea + lit;
         pe_total = etot;
-        pe_w0 = token | (remL << 8) | (remM << 16);
-        pe_w1 = ip - ref;
+        pe_tok = token;
+        pe_remL = remL;
+        pe_remM = remM;
+        pe_off = ip - ref;
         op += (int)etot;
       } else {
         op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl1, remL, src, S, anchor, true, ip - ref, nm1, remM);
@@ -473,11 +489,7 @@ last_literals:
   if (!kGuard && pe_total) {                       // the last pending sequence
     const uint32_t j = lane;
     const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
-    const uint32_t h = j == 0 ? (pe_w0 & 255u) : (j + 1u == pe_a ? ((pe_w0 >> 8) & 255u) : 255u);
-    const uint32_t t = j == pe_b ? (pe_w1 & 255u)
-                     : j == pe_b + 1u ? (pe_w1 >> 8)
-                     : (j + 1u == pe_total ? (pe_w0 >> 16) : 255u);
-    const uint32_t val = j < pe_a ? h : (j < pe_b ? lb : t);
+    const uint32_t val = pending_byte(j, lb, pe_a, pe_b, pe_total, pe_tok, pe_remL, pe_remM, pe_off);
     if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
   }
   {  // lz4.cc:627-637
