@@ -316,8 +316,11 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // checked); lanes >= 3 = search iterations 0..60.  A lane-2 match is
     // _next_match: no catch-up, no literals.
     uint32_t s = 1;                                         // lz4.cc:487
-    uint32_t t0 = 0;                                        // 1: the first chunk is a lead chunk
-    for (;;) {
+    // One sequence per call: 0 = on to the next, 1 = to the last literals,
+    // 2 = limitedOutput failure.  kLead: the search starts with a lead chunk
+    // (every sequence but a value's first), so its lane masks are constants.
+    auto sequence = [&](auto lead_c) -> int {
+      constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
       src.step(s);
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
@@ -376,7 +379,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           if ((mm | ~vm) != 0) break;                // a match, or past mflimit
         }
       }
-      if (!mm) break;
+      if (!mm) return 1;
       const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
       uint32_t ip = readlane(pk, ks);
       uint32_t ref = readlane(refk, ks);
@@ -438,9 +441,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // encoding is at most its input + lit/255 bytes, so op stays below
         // anchor + anchor/255 and both sides stay under the bound's 16 spare
         // bytes); the unguarded instantiation omits them.
-        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 0;
+        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 2;
         const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
-        if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 0;
+        if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 2;
       }
       const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
       uint32_t nl1, nm1, remL, remM;                 // remL/remM < 255 each
@@ -476,16 +479,20 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       }
       ip = ip_end;
       anchor = ip;
-      if (ip > mflimit) goto last_literals;                      // lz4.cc:597
+      if (ip > mflimit) return 1;                                // lz4.cc:597
 
       // the table fill of ip-2 (lz4.cc:600) and the test of ip run as the
       // next (lead) chunk
       s = ip + 1u;                                              // lz4.cc:623
-      t0 = 1u;
-    }
+      return 0;
+    };
+    int st = sequence(std::false_type{});
+#pragma unroll 1
+    while (st == 0) st = sequence(std::true_type{});
+    if (kGuard && st == 2) return 0;
   }
 
-last_literals:
+  // the last literals (lz4.cc:625-637)
   if (!kGuard && pe_total) {                       // the last pending sequence
     const uint32_t j = lane;
     const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
