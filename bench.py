@@ -598,10 +598,11 @@ def main() -> None:
         # several size-class launches per step: the roofline covers the step's launches together
         kc, kd = "all compress launches of the step", "all decompress launches of the step"
     else:
-        kc = ("kdb_lz4::lz4_compress_kernel<true, true, true>" if size <= 4096 else
-              "kdb_lz4::lz4_compress_big_kernel<true, false>" if size < 65547 else
+        # the launch a uniform batch of this size gets (launch_compress / launch_decompress)
+        kc = ("kdb_lz4::lz4_compress_kernel<true, true>" if size <= 4096 else
+              "kdb_lz4::lz4_compress_mixed_kernel<true>" if size < 65547 else
               "kdb_lz4::lz4_compress_big_kernel<true, true>")
-        kd = "kdb_lz4::lz4_decompress_kernel<true>" if size <= 8192 else "kdb_lz4::lz4_decompress_big_kernel<true, 4096u>"
+        kd = "kdb_lz4::lz4_decompress_kernel<true>" if size <= 8192 else "kdb_lz4::lz4_decompress_mixed_kernel<true>"
     if c_ms >= d_ms:
         dom_key, dom_name, dom_ms = "compress", kc, c_ms
     else:
