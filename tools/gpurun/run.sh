@@ -21,6 +21,8 @@
 #   hook       the flush-hook build's tests only (test_kingdb_dropin.py -k hook)
 #   wpath      KingDB's write path (kdb_db) with the reference codec, the drop-in and
 #              the flush hook, 1 M x 100 B + 128 Ki x 4 KiB, on /tmp and on /dev/shm
+#   rehearse2  the four bench workloads under torch.distributed.run with 2 ranks on this
+#              1-GPU box (ranks share the device): the N > 1 path end to end, not scaling
 #   scalar     per-call latency of CompressorLZ4::Compress/Uncompress, drop-in vs reference
 #   ab:<NAME>=<VAL>  the quick headline line with one environment knob set
 #   var:<name> A/B of kingdb_amd/var/var_<name>.so (tools/ab.py, digest-gated)
@@ -90,6 +92,13 @@ for s in "$@"; do
       for d in /tmp /dev/shm; do
         timeout -k 10 900 python -u tools/write_path_cmp.py --dir $d --out "${O}_wpath_${d//\//_}.json" > "${O}_wpath.log" 2>&1 || fail wpath $? "${O}_wpath.log"
         cat "${O}_wpath.log"
+      done ;;
+    rehearse2)
+      port=29511
+      for w in uniform mixed put get; do
+        port=$((port+1))
+        timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 --workload $w --no-cpu-baseline > "${O}_rehearse2_$w.json" 2> "${O}_rehearse2_$w.err" || fail "rehearse2 $w" $? "${O}_rehearse2_$w.err"
+        line "${O}_rehearse2_$w.json"
       done ;;
     scalar)   # per-call latency of CompressorLZ4, drop-in (GPU) vs reference codec (CPU)
       for sz in 100 4096 65536; do
