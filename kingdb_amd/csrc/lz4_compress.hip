@@ -125,21 +125,26 @@ __device__ __forceinline__ void mskor(uint32_t a, uint32_t m, uint32_t d) {
 // value (12 x 16 B stores per lane).
 struct Table12 {
   uint32_t lo_off, hi_off;   // LDS byte offsets of the two planes
+  // a lane's slot as the exchange addressed it, kept for restore(): the low
+  // byte's address, the high nibble's dword address and shift
+  struct Slot { uint32_t lo, hi, sh; };
   __device__ Table12(uint8_t* l, uint8_t* h) : lo_off(lds_off(l)), hi_off(lds_off(h)) {}
   __device__ Table12() : lo_off(0), hi_off(0) {}
   // get-then-put of every lane of the chunk, in lane order (see above)
-  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
-    const uint32_t sl = (h & 3u) << 3, sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
-    const uint32_t ml = on ? 0xffu << sl : 0u, mh = on ? 15u << sh : 0u;
+  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
+    const uint32_t sl = (h & 3u) << 3;
+    s.sh = (h & 7u) << 2;
+    s.lo = lo_off + h;
+    s.hi = hi_off + ((h >> 1) & ~3u);
+    const uint32_t ml = on ? 0xffu << sl : 0u, mh = on ? 15u << s.sh : 0u;
     uint32_t ol, oh;
-    mskor_rtn2(lo_off + (h & ~3u), ml, ((p & 0xffu) << sl) & ml, ol, hi_off + ((h >> 1) & ~3u), mh,
-               (((p >> 8) & 15u) << sh) & mh, oh);
-    return ((ol >> sl) & 0xffu) | (((oh >> sh) & 15u) << 8);
+    mskor_rtn2(s.lo & ~3u, ml, ((p & 0xffu) << sl) & ml, ol, s.hi, mh, (((p >> 8) & 15u) << s.sh) & mh, oh);
+    return ((ol >> sl) & 0xffu) | (((oh >> s.sh) & 15u) << 8);
   }
-  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const {
-    ((lds_u8*)(uintptr_t)lo_off)[h] = (uint8_t)v;
-    const uint32_t sh = (((h >> 1) & 3u) << 3) + ((h & 1u) << 2);
-    mskor(hi_off + ((h >> 1) & ~3u), 15u << sh, ((v >> 8) & 15u) << sh);
+  // v: a position < 4096
+  __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
+    ((lds_u8*)(uintptr_t)s.lo)[0] = (uint8_t)v;
+    mskor(s.hi, 15u << s.sh, (v >> 8) << s.sh);
   }
 };
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
@@ -147,38 +152,55 @@ constexpr uint32_t kTable12Bytes = 8192u + 4096u;
 // byU16 table, 8192 x u16 (values up to 65 546 bytes; positions < 65 536).
 struct Table16 {
   uint32_t off;
+  struct Slot { uint32_t h; };
   __device__ Table16(uint16_t* p) : off(lds_off(p)) {}
   __device__ Table16() : off(0) {}
-  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
+  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
+    s.h = h;
     const uint32_t sh = (h & 1u) << 4, m = on ? 0xffffu << sh : 0u;
     const uint32_t o = mskor_rtn(off + ((h & ~1u) << 1), m, ((p & 0xffffu) << sh) & m);
     return (o >> sh) & 0xffffu;
   }
-  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { ((lds_u16*)(uintptr_t)off)[h] = (uint16_t)v; }
+  __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
+    ((lds_u16*)(uintptr_t)off)[s.h] = (uint16_t)v;
+  }
 };
 
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
 struct Table32 {
   uint32_t off;
+  struct Slot { uint32_t h; };
   __device__ Table32(uint32_t* p) : off(lds_off(p)) {}
   __device__ Table32() : off(0) {}
-  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on) const {
+  __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
+    s.h = h;
     return mskor_rtn(off + (h << 2), on ? 0xffffffffu : 0u, on ? p : 0u);
   }
-  __device__ __forceinline__ void restore(uint32_t h, uint32_t v) const { ((lds_u32*)(uintptr_t)off)[h] = v; }
+  __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const { ((lds_u32*)(uintptr_t)off)[s.h] = v; }
 };
 
-// Value bytes staged in LDS (byte i at p[i]).
+// Value bytes staged in LDS (byte i at p[i]).  kUnclamped: a read outside the
+// value cannot fault (LDS), so the parse's reads whose result a lane mask
+// discards need no clamp into [0, S).
 struct LdsSrc {
+  static constexpr bool kUnclamped = true;
   const uint8_t* p;
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
   __device__ __forceinline__ uint32_t rd32(uint32_t i) const { return lds_rd32(p, i); }
+  // rd32 in two halves: the loads (issued early), then the realignment
+  struct Word { uint32_t lo, hi, sh; };
+  __device__ __forceinline__ Word rd32_issue(uint32_t i) const {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    return Word{w[i >> 2], w[(i >> 2) + 1u], i & 3u};
+  }
+  __device__ __forceinline__ static uint32_t word(const Word& w) { return __builtin_amdgcn_alignbyte(w.hi, w.lo, w.sh); }
   __device__ __forceinline__ void step(uint32_t) {}
 };
 
 // Value bytes read in place from global memory (any alignment).  An aligned
 // dword never lies on a page no needed byte lies on, so the reads cannot fault.
 struct GlobalSrc {
+  static constexpr bool kUnclamped = false;
   const uint8_t* g;
   uint32_t S;
   uint32_t keep;   // the frontier touch in flight (see step)
@@ -188,6 +210,14 @@ struct GlobalSrc {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(g + i - mis);
     return __builtin_amdgcn_alignbyte(w[mis ? 1 : 0], w[0], mis);
   }
+  // rd32 in two halves: the loads (issued early), then the realignment
+  struct Word { uint32_t lo, hi, sh; };
+  __device__ __forceinline__ Word rd32_issue(uint32_t i) const {
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3u);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(g + i - mis);
+    return Word{w[0], w[mis ? 1 : 0], mis};
+  }
+  __device__ __forceinline__ static uint32_t word(const Word& w) { return __builtin_amdgcn_alignbyte(w.hi, w.lo, w.sh); }
   // Touches the 256 bytes from p + 256 (one aligned dword per lane, clamped
   // into the value) so the search frontier is in L1/L2 before it is parsed;
   // the previous touch's dword is consumed here -- one sequence later, when
@@ -263,22 +293,31 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
-// Byte j of a pending sequence's encoding (see emit_seq): token at 0, the
-// literal-length run's last byte at a-1, literals [a, b) (lb: this lane's
-// literal byte), offset at b, b+1, the match-length run's last byte at
-// total-1, 255 elsewhere.  Later overrides win where positions coincide (a
-// missing run's "last byte" falls on the token, resp. the offset's high
-// byte); one compare-select each, no branches.
-__device__ __forceinline__ uint32_t pending_byte(uint32_t j, uint32_t lb, uint32_t a, uint32_t b, uint32_t total,
-                                                 uint32_t tok, uint32_t remL, uint32_t remM, uint32_t off) {
-  uint32_t val = 255u;
-  val = j + 1u == a ? remL : val;
-  val = j + 1u == total ? remM : val;
-  val = j == b ? (off & 255u) : val;
-  val = j == b + 1u ? (off >> 8) : val;
-  val = j == 0u ? tok : val;
-  val = (j >= a && j < b) ? lb : val;
-  return val;
+// A sequence of at most 64 encoded bytes (nearly all) in one byte store per
+// lane, byte j of the encoding on lane j: token at 0, the literal-length
+// run's last byte at a-1 (a = 1 + nl1, nl1 <= 1 here), literals [a, a+lit)
+// (lb: this lane's literal byte), offset at b, b+1 (b = a+lit), the
+// match-length run's last byte at total-1, 255 elsewhere.  The five non-255
+// header/tail bytes go in with v_writelane (later writes win where positions
+// coincide: without a run its "last byte" index falls on the token, resp.
+// the offset's high byte), so a lane's byte is one select.  The store goes
+// through a buffer resource whose range is the sequence, so lanes past it
+// are dropped by the range check: no exec mask, no 64-bit address per lane.
+__device__ __forceinline__ void store_short_seq(uint8_t* out, int pos, uint32_t total, uint32_t a, uint32_t lit,
+                                                uint32_t lb, uint32_t tok, uint32_t remL, uint32_t remM,
+                                                uint32_t off) {
+  const uint32_t lane = lane_id();
+  const uint32_t b = a + lit;
+  uint32_t hv = 255u;
+  hv = writelane(remL, a - 1u, hv);
+  hv = writelane(tok, 0u, hv);
+  hv = writelane(remM, total - 1u, hv);
+  hv = writelane(off & 255u, b, hv);
+  hv = writelane(off >> 8, b + 1u, hv);
+  const uint32_t val = lane - a < lit ? lb : hv;
+  // the range ends at the sequence's last byte: pos + total bytes from out
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, pos + (int)total, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val, r, pos + (int)lane, 0, 0);
 }
 
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
@@ -291,17 +330,17 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
   const uint32_t lane = lane_id();
   int op = 0;
   uint32_t anchor = 0;
-  // A sequence of <= 64 encoded bytes is written at the top of the next
-  // chunk: its literal read shares that chunk's first LDS round trip and its
-  // selects and store fill the wait (unguarded mode only).
-  int pe_pos = 0, pe_lbase = 0;
-  uint32_t pe_a = 0, pe_b = 0, pe_total = 0, pe_tok = 0, pe_remL = 0, pe_remM = 0, pe_off = 0;
+  // reads whose result a lane mask discards: clamped into the value only
+  // where an out-of-range read could fault (in-place values in HBM)
+  constexpr bool kFree = Src::kUnclamped;
 #define RD32(p) src.rd32(p)
 
   if (S >= kMinLength) {                                    // lz4.cc:483
     const uint32_t mflimit = S - kMfLimit;
     const uint32_t matchlimit = S - kLastLiterals;
     const uint32_t last4 = S - 4u;                          // highest position a u32 read may start
+    auto clamp4 = [&](uint32_t p) { return kFree ? p : min(p, last4); };
+    auto clamp1 = [&](uint32_t p) { return kFree ? p : min(p, S - 1u); };
     // lz4.cc:486: put(0) stores position 0 -- what an empty slot already reads as.
     //
     // After a match ending at ip the reference puts ip-2 (lz4.cc:600), then
@@ -316,6 +355,10 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // checked); lanes >= 3 = search iterations 0..60.  A lane-2 match is
     // _next_match: no catch-up, no literals.
     uint32_t s = 1;                                         // lz4.cc:487
+    // the input words of the next sequence's first chunk, read as soon as
+    // its start is known (at the end of the sequence before), so the read
+    // overlaps that sequence's byte store
+    typename Src::Word seq0 = src.rd32_issue(clamp4(s + lane));
     // One sequence per call: 0 = on to the next, 1 = to the last literals,
     // 2 = limitedOutput failure.  kLead: the search starts with a lead chunk
     // (every sequence but a value's first), so its lane masks are constants.
@@ -325,7 +368,8 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
       // mflimit without a match goes to the last literals)
-      uint32_t pk, refk, h;
+      uint32_t pk, refk;
+      typename Tab::Slot slot;
       uint64_t mm, vm;
       // the lead chunk's lane masks, per sequence (t0 != 0: lane 0 put only,
       // lane 1 dead, lane 2 valid unconditionally -- see above)
@@ -340,23 +384,18 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // valid lanes (lz4.cc:510), as a compare straight into a lane mask
         vm = (__builtin_amdgcn_uicmp(pk + 1u, mflimit, 37 /*ULE*/) | lead_or) & lead_and;
         const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
-        const uint32_t seq = RD32(min(pk, last4));
-        if (!kGuard && pe_total) {                   // the pending sequence
-          const uint32_t j = lane;
-          const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
-          const uint32_t val = pending_byte(j, lb, pe_a, pe_b, pe_total, pe_tok, pe_remL, pe_remM, pe_off);
-          if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
-          pe_total = 0;
-        }
-        h = hashp<kWide>(seq);
+        const uint32_t seq = Src::word(seq0);
+        const uint32_t h = hashp<kWide>(seq);
         // get + put of every valid lane at once, in lane order: refk is the
         // entry as the sequential loop's get at this iteration reads it
-        refk = tab.xchg(h, pk, valid);
+        refk = tab.xchg(h, pk, valid, slot);
         // the lanes whose reference matches (lz4.cc:527, 610-616), as a
         // compare straight into a lane mask (a ballot of a bool would be
         // materialised in a VGPR and compared again); byU32 adds the
-        // distance check (lz4.cc:526, 614), byU16 sizes never need it
-        mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm & lead_mm;
+        // distance check (lz4.cc:526, 614), byU16 sizes never need it.
+        // refk is a position <= mflimit of this value (the table holds
+        // nothing else), so its 4 bytes need no clamp.
+        mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) & vm & lead_mm;
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
       }
       // later chunks: no match yet and every lane valid (else: last literals)
@@ -371,10 +410,10 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           pk = search_pos_nz<kWide>(s, k);
           vm = __builtin_amdgcn_uicmp(pk + ((63u + k) >> 6), mflimit, 37 /*ULE*/);
           const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);
-          const uint32_t seq = RD32(min(pk, last4));
-          h = hashp<kWide>(seq);
-          refk = tab.xchg(h, pk, valid);
-          mm = __builtin_amdgcn_uicmp(RD32(min(refk, last4)), seq, 32 /*EQ*/) & vm;
+          const uint32_t seq = RD32(clamp4(pk));
+          const uint32_t h = hashp<kWide>(seq);
+          refk = tab.xchg(h, pk, valid, slot);
+          mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) & vm;
           if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
           if ((mm | ~vm) != 0) break;                // a match, or past mflimit
         }
@@ -387,35 +426,25 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // per slot, the lowest such lane holds the entry as lanes <= ks left it
       // -- its refk is a position <= ip (positions grow with the lane; entries
       // from before the chunk are smaller still)
-      if (__builtin_amdgcn_inverse_ballot_w64(vm) && lane > ks && refk <= ip) tab.restore(h, refk);
+      if (__builtin_amdgcn_inverse_ballot_w64(vm & ~mask_le(ks)) && refk <= ip) tab.restore(slot, refk);
       const bool catchup = ks != next_lane;       // a lane-2 match of a lead chunk is _next_match
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
-      uint32_t c, ml;
+      uint32_t c, ml, ip_end;
       {
         const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
         const uint32_t rem = matchlimit - (ip + kMinMatch);
-        // the reads go out first (addresses clamped into the value, lanes
-        // past lim / rem read something harmless); the masks are built while
-        // they are in flight
-        const uint32_t a0 = src.u8(min(ip - 1u - lane, S - 1u)), b0 = src.u8(min(ref - 1u - lane, S - 1u));
-        const uint32_t a1 = src.u8(min(ip + kMinMatch + lane, S - 1u));
-        const uint32_t b1 = src.u8(min(ref + kMinMatch + lane, S - 1u));
+        // the reads go out first (lanes past lim / rem read something
+        // harmless, clamped into the value only in HBM); the masks are
+        // built while they are in flight
+        const uint32_t a0 = src.u8(clamp1(ip - 1u - lane)), b0 = src.u8(clamp1(ref - 1u - lane));
+        const uint32_t a1 = src.u8(clamp1(ip + kMinMatch + lane));
+        const uint32_t b1 = src.u8(clamp1(ref + kMinMatch + lane));
         const uint64_t clm = __builtin_amdgcn_uicmp(lane, lim, 36 /*ULT*/);   // lanes < lim
         const uint64_t mlm = __builtin_amdgcn_uicmp(lane, rem, 36 /*ULT*/);   // lanes < rem
         // compares straight into lane masks; lanes past lim / rem vote false
         c = first_zero(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & clm);
         ml = first_zero(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
-        if (c == 64u) {
-#pragma unroll 1
-          for (;;) {
-            const bool l2 = lane < lim - c;
-            const uint32_t x = src.u8(l2 ? ip - c - 1u - lane : 0u), y = src.u8(l2 ? ref - c - 1u - lane : 0u);
-            const uint32_t d = first_zero(ballot(l2 && x == y));
-            c += d;
-            if (d < 64u) break;
-          }
-        }
         if (ml == 64u) {
 #pragma unroll 1
           for (;;) {
@@ -427,11 +456,24 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
             if (d < 64u) break;
           }
         }
+        // the match ends at ip_end whatever the catch-up
+        ip_end = ip + kMinMatch + ml;
+        s = ip_end + 1u;                                        // lz4.cc:623
+        if (c == 64u) {
+#pragma unroll 1
+          for (;;) {
+            const bool l2 = lane < lim - c;
+            const uint32_t x = src.u8(l2 ? ip - c - 1u - lane : 0u), y = src.u8(l2 ? ref - c - 1u - lane : 0u);
+            const uint32_t d = first_zero(ballot(l2 && x == y));
+            c += d;
+            if (d < 64u) break;
+          }
+        }
       }
-      const uint32_t ip_end = ip + kMinMatch + ml;  // independent of the catch-up
       ip -= c;
       ref -= c;
       ml += c;
+      const uint32_t moff = ip - ref;
 
       // ======== token + literals (lz4.cc:535-550), offset (554), match length (580-592)
       const uint32_t lit = ip - anchor;
@@ -463,28 +505,24 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       }
       const uint32_t ea = 1u + nl1;
       const uint32_t etot = ea + lit + 2u + nm1;
+      const int seq_op = op;
+      const uint32_t seq_anchor = anchor;
+      op += (int)etot;
+      anchor = ip_end;
+      // lz4.cc:597; else the table fill of ip-2 (lz4.cc:600) and the test of
+      // ip run as the next (lead) chunk, positions ip-2+lane (seq0 above)
+      const int st = ip_end > mflimit ? 1 : 0;
+      // the next sequence's input words go out before this sequence's bytes,
+      // whose literal read shares their round trip (measured a little faster
+      // than issuing them right after the match length)
+      seq0 = src.rd32_issue(clamp4(s - 3u + lane));
       if (!kGuard && etot <= 64u) {
-        pe_pos = op;
-        pe_lbase = (int)anchor - (int)ea;
-        pe_a = ea;
-        pe_b = ea + lit;
-        pe_total = etot;
-        pe_tok = token;
-        pe_remL = remL;
-        pe_remM = remM;
-        pe_off = ip - ref;
-        op += (int)etot;
+        const uint32_t lb = src.u8(clamp1(seq_anchor - ea + lane));
+        store_short_seq(out, seq_op, etot, ea, lit, lb, token, remL, remM, moff);
       } else {
-        op += emit_seq<kGuard>(out, out_cap, op, token, lit, nl1, remL, src, S, anchor, true, ip - ref, nm1, remM);
+        emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, seq_anchor, true, moff, nm1, remM);
       }
-      ip = ip_end;
-      anchor = ip;
-      if (ip > mflimit) return 1;                                // lz4.cc:597
-
-      // the table fill of ip-2 (lz4.cc:600) and the test of ip run as the
-      // next (lead) chunk
-      s = ip + 1u;                                              // lz4.cc:623
-      return 0;
+      return st;
     };
     int st = sequence(std::false_type{});
 #pragma unroll 1
@@ -492,14 +530,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     if (kGuard && st == 2) return 0;
   }
 
-  // the last literals (lz4.cc:625-637)
-  if (!kGuard && pe_total) {                       // the last pending sequence
-    const uint32_t j = lane;
-    const uint32_t lb = src.u8((uint32_t)min(max(pe_lbase + (int)j, 0), (int)S - 1));
-    const uint32_t val = pending_byte(j, lb, pe_a, pe_b, pe_total, pe_tok, pe_remL, pe_remM, pe_off);
-    if (j < pe_total) out[pe_pos + (int)j] = (uint8_t)val;
-  }
-  {  // lz4.cc:627-637
+  {  // the last literals (lz4.cc:625-637)
     const uint32_t run = S - anchor;
     if (kGuard && op + (int)run + 1 + (int)((run + 255u - kRunMask) / 255u) > cap) return 0;
     const uint32_t nl1 = run_bytes(run);

@@ -40,6 +40,13 @@ __device__ __forceinline__ uint32_t readlane(uint32_t x, uint32_t l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)l);
 }
 
+// v_writelane_b32: `old` with lane l replaced by the uniform v (clang has no
+// builtin for it; the LLVM intrinsic is declared directly)
+extern "C" __device__ int kdb_llvm_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t l, uint32_t old) {
+  return (uint32_t)kdb_llvm_writelane((int)v, (int)l, (int)old);
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 // Lanes-below / lanes-up-to masks (lane in 0..63; 2ull<<63 wraps to 0 -> ~0).
@@ -118,6 +125,9 @@ __host__ __device__ __forceinline__ uint32_t compress_bound(uint32_t n) {
 
 // Unaligned little-endian u32 at byte offset b of a 16B-aligned LDS buffer
 // that is readable for 4 bytes past b+3 (two aligned dwords + v_alignbyte).
+// (A single unaligned ds_read_b32 returns the same bytes on gfx950 --
+// tools/probe/lds_unaligned.hip -- but measured far slower: compress 11.3 ->
+// 13.8 ms, decompress 3.6 -> 5.6 ms at 1 Mi x 4 KiB.)
 __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t b) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds);
   uint32_t q = b >> 2;
