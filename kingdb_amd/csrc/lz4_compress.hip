@@ -127,7 +127,7 @@ struct Table12 {
   uint32_t lo_off, hi_off;   // LDS byte offsets of the two planes
   // a lane's slot as the exchange addressed it, kept for restore(): the low
   // byte's address, the high nibble's dword address and shift
-  struct Slot { uint32_t lo, hi, sh; };
+  struct Slot { uint32_t lo, hi, sh, mh; };
   __device__ Table12(uint8_t* l, uint8_t* h) : lo_off(lds_off(l)), hi_off(lds_off(h)) {}
   __device__ Table12() : lo_off(0), hi_off(0) {}
   // get-then-put of every lane of the chunk, in lane order (see above)
@@ -136,15 +136,16 @@ struct Table12 {
     s.sh = (h & 7u) << 2;
     s.lo = lo_off + h;
     s.hi = hi_off + ((h >> 1) & ~3u);
-    const uint32_t ml = on ? 0xffu << sl : 0u, mh = on ? 15u << s.sh : 0u;
+    const uint32_t ml = on ? 0xffu << sl : 0u;
+    s.mh = on ? 15u << s.sh : 0u;
     uint32_t ol, oh;
-    mskor_rtn2(s.lo & ~3u, ml, ((p & 0xffu) << sl) & ml, ol, s.hi, mh, (((p >> 8) & 15u) << s.sh) & mh, oh);
+    mskor_rtn2(s.lo & ~3u, ml, ((p & 0xffu) << sl) & ml, ol, s.hi, s.mh, (((p >> 8) & 15u) << s.sh) & s.mh, oh);
     return ((ol >> sl) & 0xffu) | (((oh >> s.sh) & 15u) << 8);
   }
-  // v: a position < 4096
+  // v: a position < 4096; only lanes whose exchange was on (mh = their nibble mask)
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
     ((lds_u8*)(uintptr_t)s.lo)[0] = (uint8_t)v;
-    mskor(s.hi, 15u << s.sh, (v >> 8) << s.sh);
+    mskor(s.hi, s.mh, (v >> 8) << s.sh);
   }
 };
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
@@ -382,7 +383,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       {
         pk = s - o3 + lane;
         // valid lanes (lz4.cc:510), as a compare straight into a lane mask
-        vm = (__builtin_amdgcn_uicmp(pk + 1u, mflimit, 37 /*ULE*/) | lead_or) & lead_and;
+        // pk + 1 <= mflimit as a compare of the lane index with a scalar
+        // bound (no pk in the chain: s <= mflimit + 1, so it is >= -2)
+        vm = (__builtin_amdgcn_sicmp((int)lane, (int)(mflimit - 1u - s + o3), 41 /*SLE*/) | lead_or) & lead_and;
         const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
         const uint32_t seq = Src::word(seq0);
         const uint32_t h = hashp<kWide>(seq);
@@ -443,9 +446,12 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         const uint64_t clm = __builtin_amdgcn_uicmp(lane, lim, 36 /*ULT*/);   // lanes < lim
         const uint64_t mlm = __builtin_amdgcn_uicmp(lane, rem, 36 /*ULT*/);   // lanes < rem
         // compares straight into lane masks; lanes past lim / rem vote false
-        c = first_zero(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & clm);
-        ml = first_zero(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
-        if (ml == 64u) {
+        const int c0 = first_zero_or_neg(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & clm);
+        const int ml0 = first_zero_or_neg(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
+        c = (uint32_t)c0;
+        ml = (uint32_t)ml0;
+        if (ml0 < 0) {
+          ml = 64u;
 #pragma unroll 1
           for (;;) {
             const bool l2 = lane < rem - ml;
@@ -459,7 +465,8 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // the match ends at ip_end whatever the catch-up
         ip_end = ip + kMinMatch + ml;
         s = ip_end + 1u;                                        // lz4.cc:623
-        if (c == 64u) {
+        if (c0 < 0) {
+          c = 64u;
 #pragma unroll 1
           for (;;) {
             const bool l2 = lane < lim - c;

@@ -66,11 +66,11 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
   in_off = uni(in_off);
   const int iend = unii(csize), oend = unii(osize);
   const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
-  // fast-path bounds: a sequence starting at ip <= far_ip (<= 62 header and
-  // literal bytes, then 3 more) is not the last by input; at op <= far_op its
-  // literals stay under oexit and its match (<= 273 bytes) under oend - 5
-  const int far_ip = iend - (int)(2 + 1 + kLastLiterals) - 62;
-  const int far_op = min(oexit - 60, oend - (int)kLastLiterals - 60 - 273);
+  // fast-path bounds, per sequence and exact (lz4.cc:930-933, 1024): it is not
+  // the last if its literals end at ip <= iend8 and op <= oexit; its match
+  // must end at or before oend5
+  const int iend8 = iend - (int)(2 + 1 + kLastLiterals);
+  const int oend5 = oend - (int)kLastLiterals;
   const uint8_t* in = lds_in + in_off;
   Window wd{reinterpret_cast<const uint32_t*>(lds_in), 0u, 0u};
   wd.load(in_off);
@@ -101,16 +101,23 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // token word and the length arithmetic -- in VGPRs (vgpr(): every lane
       // holds the same value) and only the loop and copy decisions go
       // through the scalar unit (readfirstlane + one compare).  The bounds
-      // are folded into one "far from both ends" test per sequence -- ip <=
-      // far_ip, op <= far_op make the not-last and output checks of any fast
-      // sequence true (lit <= 60, mlen <= 273) -- and the rest are sign bits
-      // of plain integer expressions.
+      // are the reference's own not-last and match-end conditions for this
+      // sequence (so only the true last sequence leaves the fast path; a
+      // worst-case "far from both ends" test had sent the last ~330 output
+      // bytes of every value through the general path), folded with the
+      // rest into sign bits of plain integer expressions, one decision.
       //
       // The next sequence's literal load goes out as soon as its token is
       // known (v_readlane of this one's load), before this sequence's match
       // copy, so the two LDS round trips of a sequence overlap.
+      // The match half of a sequence (token low nibble, offset, match-length
+      // byte, next token's lane) is computed from SGPRs -- the v_readlane
+      // results are scalar already -- and only the literal half and the
+      // positions stay on the VALU: 3.60 -> 3.56 ms at 1 Mi x 4 KiB (the whole
+      // sequence on the scalar unit measured 4.44, the header too 3.87).
       int vip = vgpr(ip), vop = vgpr(op);
       uint32_t vq = vgpr(q);
+      uint32_t sq = q;                     // the token word in an SGPR
       // a sequence's literal-run header from its token word tq at tip: lx (a
       // literal-length byte follows), xl (its value or 0), lit, ls (first literal)
       int lx, xl, lit, ls;
@@ -131,19 +138,23 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
 #pragma unroll 1
       for (;;) {
-        const int mn = (int)(vq & 0xffu) & (int)kMlMask;
+        const int mn = (int)(sq & 0xffu) & (int)kMlMask;
+        const int slit = unii(lit);
         const int opl = vop + lit;
-        const uint32_t w = readlane(v, (uint32_t)unii(lit) & 63u);   // offset, match-length byte
+        const uint32_t w = readlane(v, (uint32_t)slit & 63u);   // offset, match-length byte
         const int e = (int)((w >> 16) & 0xffu);
         const int off = (int)(w & 0xffffu);
         const int mx = (mn + 1) >> 4;                             // a match-length byte follows
         const int xm = e & -mx;
         const int mlen = mn + xm + (int)kMinMatch;
         // far from both ends, <= 60 literals, ref >= 0, one match-length byte
-        if (unii((far_ip - vip) | (far_op - vop) | (45 - xl) | (opl - off) | (254 - xm)) < 0) break;
+        if ((unii((iend8 - ls - lit) | (oexit - opl) | (45 - xl) | (opl - off) | ((oend5 - mlen) - opl)) |
+             (254 - xm)) < 0)
+          break;
         out[vop + (int)lane] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
-        const int nt = lit + 2 + mx;                              // next token's lane (<= 63)
-        vq = vgpr(readlane(v, (uint32_t)unii(nt)));
+        const int nt = slit + 2 + mx;                             // next token's lane (<= 63)
+        sq = readlane(v, (uint32_t)nt);
+        vq = vgpr(sq);
         vip = ls + nt;
         header(vq, vip);
         v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));   // the next sequence's literals

@@ -58,6 +58,13 @@ __device__ __forceinline__ uint32_t first_zero(uint64_t m) {
   uint64_t z = ~m;
   return z ? (uint32_t)__builtin_ctzll(z) : 64u;
 }
+// The same as one s_ff0_i32_b64 (the compiler's ctz(~m) with the "none" case
+// is s_not + s_ff1 + s_min): the index of the first zero bit, -1 if none.
+__device__ __forceinline__ int first_zero_or_neg(uint64_t m) {
+  int r;
+  asm("s_ff0_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+  return r;
+}
 
 // Dynamic work distribution of the persistent kernels.  Lane 0 claims `batch`
 // consecutive value indices with one device-scope atomic.  A single counter
