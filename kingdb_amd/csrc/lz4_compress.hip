@@ -377,7 +377,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       const uint64_t lead_or = t0 ? 5ull : 0ull, lead_and = t0 ? ~2ull : ~0ull;
       const uint64_t lead_mm = t0 ? ~1ull : ~0ull, lead_full = t0 ? 2ull : 0ull;
       const uint32_t o3 = 3u * t0;
-      uint32_t next_lane = t0 ? 2u : 64u;             // a match on this lane is _next_match
       // First chunk (nearly every sequence's only one): step(k) = 1 for k <= 64,
       // so its positions are s-o3+lane.
       {
@@ -404,7 +403,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // later chunks: no match yet and every lane valid (else: last literals)
       if ((mm | ~(vm | lead_full)) == 0) {
         uint32_t kb = 0;
-        next_lane = 64u;
 #pragma unroll 1
         for (;;) {
           kb += 64u;
@@ -430,12 +428,13 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // -- its refk is a position <= ip (positions grow with the lane; entries
       // from before the chunk are smaller still)
       if (__builtin_amdgcn_inverse_ballot_w64(vm & ~mask_le(ks)) && refk <= ip) tab.restore(slot, refk);
-      const bool catchup = ks != next_lane;       // a lane-2 match of a lead chunk is _next_match
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml, ip_end;
       {
-        const uint32_t lim = catchup ? min(ip - anchor, ref) : 0u;
+        // catch-up bound (lz4.cc:531: ip > anchor, ref > base): 0 for a
+        // lane-2 match of a lead chunk (ip == anchor), the _next_match path
+        const uint32_t lim = min(ip - anchor, ref);
         const uint32_t rem = matchlimit - (ip + kMinMatch);
         // the reads go out first (lanes past lim / rem read something
         // harmless, clamped into the value only in HBM); the masks are

@@ -39,6 +39,20 @@ __device__ __forceinline__ uint32_t vgpr(uint32_t x) {
   return x;
 }
 
+// Unaligned u32 at an absolute LDS byte address (two aligned dwords +
+// v_alignbyte): the base is folded into the address, so no add of the LDS
+// buffer's (link-time) base per read.
+__device__ __forceinline__ uint32_t lds_rd32_at(uint32_t a) {
+  typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+  const lds_cu32* w = (lds_cu32*)(uintptr_t)(a & ~3u);
+  return __builtin_amdgcn_alignbyte(w[1], w[0], a & 3u);
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  uint32_t o = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+  asm volatile("" : "+s"(o));
+  return o;
+}
+
 // 256-byte window over the staged block (LDS byte coordinates).
 struct Window {
   const uint32_t* w32;   // LDS buffer as dwords
@@ -135,7 +149,8 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // fast-path test (its address is inside the staged block plus the
       // window slack for any token; a sequence that fails the test never
       // uses it), so both tests are one scalar decision.
-      uint32_t v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));
+      const uint32_t in_abs = lds_addr(lds_in) + in_off;
+      uint32_t v = lds_rd32_at(in_abs + (uint32_t)(ls + (int)lane));
 #pragma unroll 1
       for (;;) {
         const int mn = (int)(sq & 0xffu) & (int)kMlMask;
@@ -157,7 +172,7 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         vq = vgpr(sq);
         vip = ls + nt;
         header(vq, vip);
-        v = lds_rd32(lds_in, in_off + (uint32_t)(ls + (int)lane));   // the next sequence's literals
+        v = lds_rd32_at(in_abs + (uint32_t)(ls + (int)lane));   // the next sequence's literals
         const int ref = opl - off;
         asm volatile("" ::: "memory");
         if (unii(off - min(mlen, 64)) < 0) {
