@@ -495,15 +495,15 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       }
       const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
       uint32_t nl1, nm1, remL, remM;                 // remL/remM < 255 each
-      if (max(lit, ml) < 270u) {
-        // at most one run byte each (almost every sequence): (n+241)>>8 is
-        // (n >= 15), the byte n-15; without a run its "last byte" index falls
-        // on a byte of higher precedence, so any 8-bit value does
-        nl1 = (lit + 241u) >> 8;
-        nm1 = (ml + 241u) >> 8;
-        remL = (lit - 15u) & 255u;
-        remM = (ml - 15u) & 255u;
-      } else {
+      // at most one run byte each (almost every sequence): (n+241)>>8 is
+      // (n >= 15), the byte n-15; without a run its "last byte" index falls
+      // on a byte of higher precedence, so any 8-bit value does.  Longer runs
+      // override (an if without an else: one scalar branch, no flags)
+      nl1 = (lit + 241u) >> 8;
+      nm1 = (ml + 241u) >> 8;
+      remL = (lit - 15u) & 255u;
+      remM = (ml - 15u) & 255u;
+      if (max(lit, ml) >= 270u) {
         nl1 = run_bytes(lit);
         nm1 = run_bytes(ml);
         remL = run_last(lit, nl1);
@@ -522,12 +522,14 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // whose literal read shares their round trip (measured a little faster
       // than issuing them right after the match length)
       seq0 = src.rd32_issue(clamp4(s - 3u + lane));
-      if (!kGuard && etot <= 64u) {
+      // a sequence of <= 64 bytes in one store (its range 0 -- nothing stored
+      // -- for a longer one, which emit_seq writes): no if/else around it
+      if (!kGuard) {
         const uint32_t lb = src.u8(clamp1(seq_anchor - ea + lane));
-        store_short_seq(out, seq_op, etot, ea, lit, lb, token, remL, remM, moff);
-      } else {
-        emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, seq_anchor, true, moff, nm1, remM);
+        store_short_seq(out, seq_op, etot <= 64u ? etot : 0u, ea, lit, lb, token, remL, remM, moff);
       }
+      if (kGuard || etot > 64u)
+        emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, seq_anchor, true, moff, nm1, remM);
       return st;
     };
     int st = sequence(std::false_type{});

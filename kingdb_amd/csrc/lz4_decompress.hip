@@ -175,31 +175,37 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         v = lds_rd32_at(in_abs + (uint32_t)(ls + (int)lane));   // the next sequence's literals
         const int ref = opl - off;
         asm volatile("" ::: "memory");
-        if (unii(off - min(mlen, 64)) < 0) {
+        // the match's first 64-byte step as a plain copy, unconditionally
+        // (mlen >= 4; lanes past mlen write the not-yet-produced tail); only
+        // an overlapping match (offset < its first step: periodic, or offset
+        // 0) or one longer than a step takes the branch, which for an
+        // overlapping match rewrites the whole match (a plain copy may have
+        // read bytes of this step before they were written)
+        const uint8_t b0 = out[ref + (int)lane];
+        out[opl + (int)lane] = b0;
+        asm volatile("" ::: "memory");
+        if (((off - min(mlen, 64)) | (64 - mlen)) < 0) {
           const int steps = unii(mlen);
-          if (unii(off) > 0) {                    // periodic (see the general path)
-            const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-            const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+          if (off - min(mlen, 64) < 0) {
+            if (off > 0) {                        // periodic (see the general path)
+              const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+              const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
 #pragma unroll 1
-            for (int i = 0; i < steps; i += 64) {
-              const uint8_t b = out[ref + i + rr];
-              out[opl + i + (int)lane] = b;
+              for (int i = 0; i < steps; i += 64) {
+                const uint8_t b = out[ref + i + rr];
+                out[opl + i + (int)lane] = b;
+              }
+            } else {                              // offset 0: zeros (see the general path)
+#pragma unroll 1
+              for (int i = 0; i < steps; i += 64) out[opl + i + (int)lane] = 0;
             }
-          } else {                                // offset 0: zeros (see the general path)
+          } else {
 #pragma unroll 1
-            for (int i = 0; i < steps; i += 64) out[opl + i + (int)lane] = 0;
-          }
-        } else {
-          // the first 64-byte step unconditionally (mlen >= 4), the rest only for long matches
-          const uint8_t b0 = out[ref + (int)lane];
-          out[opl + (int)lane] = b0;
-          asm volatile("" ::: "memory");
-          const int steps = unii(mlen);
-#pragma unroll 1
-          for (int i = 64; i < steps; i += 64) {
-            const uint8_t b = out[ref + i + (int)lane];
-            out[opl + i + (int)lane] = b;
-            asm volatile("" ::: "memory");
+            for (int i = 64; i < steps; i += 64) {
+              const uint8_t b = out[ref + i + (int)lane];
+              out[opl + i + (int)lane] = b;
+              asm volatile("" ::: "memory");
+            }
           }
         }
         asm volatile("" ::: "memory");
