@@ -96,18 +96,6 @@ __device__ __forceinline__ uint32_t lds_off(const void* p) {
   return o;
 }
 
-// Two masked-or exchanges with return, one wait: the compiler does not count
-// lgkmcnt for inline asm, so the asm waits for its own results.
-__device__ __forceinline__ void mskor_rtn2(uint32_t a0, uint32_t m0, uint32_t d0, uint32_t& r0, uint32_t a1,
-                                           uint32_t m1, uint32_t d1, uint32_t& r1) {
-  asm volatile(
-      "ds_mskor_rtn_b32 %0, %2, %3, %4\n\t"
-      "ds_mskor_rtn_b32 %1, %5, %6, %7\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(r0), "=&v"(r1)
-      : "v"(a0), "v"(m0), "v"(d0), "v"(a1), "v"(m1), "v"(d1)
-      : "memory");
-}
 __device__ __forceinline__ uint32_t mskor_rtn(uint32_t a, uint32_t m, uint32_t d) {
   uint32_t r;
   asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r) : "v"(a), "v"(m), "v"(d)
@@ -122,30 +110,45 @@ __device__ __forceinline__ void mskor(uint32_t a, uint32_t m, uint32_t d) {
 // the low bytes (8192 x u8) and the high nibbles (4096 x u8, two per byte),
 // 12 KiB instead of 16 -- 16 KiB of LDS per value with its bytes, so 10
 // values per CU (the parse is latency-bound: occupancy is speed).  Cleared per
-// value (12 x 16 B stores per lane).
+// value (12 x 16 B stores per lane).  The layout is fixed (the kernels that
+// use it have one static LDS array, at LDS address 0): the value at [0, 4096),
+// the low bytes at kT12Lo, the high nibbles at kT12Hi -- both planes are
+// addressed through the instructions' offset fields, and the value's bytes
+// need no base, so no address of the parse carries an add for a region base.
+#define KDB_T12_LO 4096
+#define KDB_T12_HI 12288
+constexpr uint32_t kT12Lo = KDB_T12_LO, kT12Hi = KDB_T12_HI;
+static_assert(kT12Lo == 4096u && kT12Hi == kT12Lo + 8192u, "value, then the 8 KiB low-byte plane, then the nibbles");
+#define KDB_STR2(x) #x
+#define KDB_STR(x) KDB_STR2(x)
 struct Table12 {
-  uint32_t lo_off, hi_off;   // LDS byte offsets of the two planes
   // a lane's slot as the exchange addressed it, kept for restore(): the low
-  // byte's address, the high nibble's dword address and shift
+  // byte's index, the high nibble's dword address (in its plane) and shift
   struct Slot { uint32_t lo, hi, sh, mh; };
-  __device__ Table12(uint8_t* l, uint8_t* h) : lo_off(lds_off(l)), hi_off(lds_off(h)) {}
-  __device__ Table12() : lo_off(0), hi_off(0) {}
   // get-then-put of every lane of the chunk, in lane order (see above)
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
     const uint32_t sl = (h & 3u) << 3;
     s.sh = (h & 7u) << 2;
-    s.lo = lo_off + h;
-    s.hi = hi_off + ((h >> 1) & ~3u);
+    s.lo = h;
+    s.hi = (h >> 1) & ~3u;
     const uint32_t ml = on ? 0xffu << sl : 0u;
     s.mh = on ? 15u << s.sh : 0u;
     uint32_t ol, oh;
-    mskor_rtn2(s.lo & ~3u, ml, ((p & 0xffu) << sl) & ml, ol, s.hi, s.mh, (((p >> 8) & 15u) << s.sh) & s.mh, oh);
-    return ((ol >> sl) & 0xffu) | (((oh >> s.sh) & 15u) << 8);
+    asm volatile(
+        "ds_mskor_rtn_b32 %0, %2, %3, %4 offset:" KDB_STR(KDB_T12_LO) "\n\t"
+        "ds_mskor_rtn_b32 %1, %5, %6, %7 offset:" KDB_STR(KDB_T12_HI) "\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(ol), "=&v"(oh)
+        : "v"(h & ~3u), "v"(ml), "v"(((p & 0xffu) << sl) & ml), "v"(s.hi), "v"(s.mh),
+          "v"((((p >> 8) & 15u) << s.sh) & s.mh)
+        : "memory");
+    return (__builtin_amdgcn_ubfe(oh, s.sh, 4) << 8) | __builtin_amdgcn_ubfe(ol, sl, 8);
   }
   // v: a position < 4096; only lanes whose exchange was on (mh = their nibble mask)
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
-    ((lds_u8*)(uintptr_t)s.lo)[0] = (uint8_t)v;
-    mskor(s.hi, s.mh, (v >> 8) << s.sh);
+    ((lds_u8*)(uintptr_t)(s.lo + kT12Lo))[0] = (uint8_t)v;
+    asm volatile("ds_mskor_b32 %0, %1, %2 offset:" KDB_STR(KDB_T12_HI) ::"v"(s.hi), "v"(s.mh), "v"((v >> 8) << s.sh)
+                 : "memory");
   }
 };
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
@@ -360,8 +363,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // its start is known (at the end of the sequence before), so the read
     // overlaps that sequence's byte store
     typename Src::Word seq0 = src.rd32_issue(clamp4(s + lane));
-    // One sequence per call: 0 = on to the next, 1 = to the last literals,
-    // 2 = limitedOutput failure.  kLead: the search starts with a lead chunk
+    // One sequence per call: 0 = a match was encoded (on to the next unless
+    // it ended past mflimit), 1 = no match (to the last literals), 2 =
+    // limitedOutput failure.  kLead: the search starts with a lead chunk
     // (every sequence but a value's first), so its lane masks are constants.
     auto sequence = [&](auto lead_c) -> int {
       constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
@@ -401,7 +405,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
       }
       // later chunks: no match yet and every lane valid (else: last literals)
-      if ((mm | ~(vm | lead_full)) == 0) {
+      if (__builtin_expect((mm | ~(vm | lead_full)) == 0, 0)) {
         uint32_t kb = 0;
 #pragma unroll 1
         for (;;) {
@@ -419,7 +423,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           if ((mm | ~vm) != 0) break;                // a match, or past mflimit
         }
       }
-      if (!mm) return 1;
+      if (__builtin_expect(!mm, 0)) return 1;
       const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
       uint32_t ip = readlane(pk, ks);
       uint32_t ref = readlane(refk, ks);
@@ -449,7 +453,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         const int ml0 = first_zero_or_neg(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
         c = (uint32_t)c0;
         ml = (uint32_t)ml0;
-        if (ml0 < 0) {
+        if (__builtin_expect(ml0 < 0, 0)) {
           ml = 64u;
 #pragma unroll 1
           for (;;) {
@@ -464,7 +468,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // the match ends at ip_end whatever the catch-up
         ip_end = ip + kMinMatch + ml;
         s = ip_end + 1u;                                        // lz4.cc:623
-        if (c0 < 0) {
+        if (__builtin_expect(c0 < 0, 0)) {
           c = 64u;
 #pragma unroll 1
           for (;;) {
@@ -503,7 +507,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       nm1 = (ml + 241u) >> 8;
       remL = (lit - 15u) & 255u;
       remM = (ml - 15u) & 255u;
-      if (max(lit, ml) >= 270u) {
+      if (__builtin_expect(max(lit, ml) >= 270u, 0)) {
         nl1 = run_bytes(lit);
         nm1 = run_bytes(ml);
         remL = run_last(lit, nl1);
@@ -515,9 +519,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       const uint32_t seq_anchor = anchor;
       op += (int)etot;
       anchor = ip_end;
-      // lz4.cc:597; else the table fill of ip-2 (lz4.cc:600) and the test of
-      // ip run as the next (lead) chunk, positions ip-2+lane (seq0 above)
-      const int st = ip_end > mflimit ? 1 : 0;
       // the next sequence's input words go out before this sequence's bytes,
       // whose literal read shares their round trip (measured a little faster
       // than issuing them right after the match length)
@@ -528,13 +529,22 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         const uint32_t lb = src.u8(clamp1(seq_anchor - ea + lane));
         store_short_seq(out, seq_op, etot <= 64u ? etot : 0u, ea, lit, lb, token, remL, remM, moff);
       }
-      if (kGuard || etot > 64u)
+      if (kGuard || __builtin_expect(etot > 64u, 0))
         emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, seq_anchor, true, moff, nm1, remM);
-      return st;
+      return 0;
     };
     int st = sequence(std::false_type{});
+    // lz4.cc:597 (the match ended past mflimit: the last literals); else the
+    // table fill of ip-2 (lz4.cc:600) and the test of ip run as the next
+    // (lead) chunk, positions ip-2+lane (seq0 above).  The test is made here,
+    // at the branch, so no flag carries it across the sequence's byte store.
+    if (st == 0) {
 #pragma unroll 1
-    while (st == 0) st = sequence(std::true_type{});
+      while (anchor <= mflimit) {
+        st = sequence(std::true_type{});
+        if (__builtin_expect(st != 0, 0)) break;
+      }
+    }
     if (kGuard && st == 2) return 0;
   }
 
@@ -582,15 +592,17 @@ __device__ __forceinline__ void values_loop(
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
   constexpr uint32_t kTabBytes = kSmall ? kTable12Bytes : kTableBytes;
-  uint8_t* s_in = smem + kTabBytes;      // value bytes [0, S), 16B-aligned
+  // kSmall: the value at [0, 4 KiB), Table12 after it (see Table12); else
+  // Table16, then the value
+  uint8_t* s_in = kSmall ? smem : smem + kTabBytes;      // value bytes [0, S), 16B-aligned
+  uint8_t* s_tab = kSmall ? smem + kT12Lo : smem;
   const uint4 z4 = make_uint4(0, 0, 0, 0);
 
   using Tab = typename std::conditional<kSmall, Table12, Table16>::type;
   Tab tab;
-  if constexpr (kSmall) tab = Table12(smem, smem + 8192u);
-  else tab = Table16(tab16);
+  if constexpr (!kSmall) tab = Table16(tab16);
   if (kSmall) {
-    for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(smem)[i] = z4;
+    for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(s_tab)[i] = z4;
   }
 
   // register prefetch (kSmall): the next value's realigned 16-byte chunks
@@ -673,7 +685,7 @@ __device__ __forceinline__ void values_loop(
     }
     if (kSmall) {                                // a zeroed table per value (lz4.cc:669)
 #pragma unroll
-      for (uint32_t k = 0; k < kTabBytes / 1024u; ++k) reinterpret_cast<uint4*>(smem)[lane + 64u * k] = z4;
+      for (uint32_t k = 0; k < kTabBytes / 1024u; ++k) reinterpret_cast<uint4*>(s_tab)[lane + 64u * k] = z4;
     }
     __syncthreads();
     v = vn;
@@ -689,8 +701,9 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
     uint32_t cls, uint32_t nq) {
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
-  // kSmall: a fixed LDS layout, so every LDS address is a constant offset (a
-  // dynamic allocation's base costs a v_add per address)
+  // kSmall: a fixed LDS layout at LDS address 0 (the kernel's only LDS
+  // array), so every LDS address is a constant offset (a dynamic
+  // allocation's base costs a v_add per address)
   constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u : 16u;
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
