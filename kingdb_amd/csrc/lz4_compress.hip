@@ -301,27 +301,41 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
 // lane, byte j of the encoding on lane j: token at 0, the literal-length
 // run's last byte at a-1 (a = 1 + nl1, nl1 <= 1 here), literals [a, a+lit)
 // (lb: this lane's literal byte), offset at b, b+1 (b = a+lit), the
-// match-length run's last byte at total-1, 255 elsewhere.  The five non-255
-// header/tail bytes go in with v_writelane (later writes win where positions
-// coincide: without a run its "last byte" index falls on the token, resp.
-// the offset's high byte), so a lane's byte is one select.  The store goes
+// match-length run's last byte at total-1, 255 elsewhere.  The token, remL
+// and remM go in with v_writelane (remL always at lane 1: with no run, lane 1
+// is a literal or the offset's low byte, which take precedence), the offset's
+// two bytes are shifted out of the offset by each lane's distance from b, so
+// a lane's byte is two selects and only remM's lane goes through m0 (each
+// writelane at a variable lane costs a scalar m0 write: the CU's one scalar
+// unit, shared by its waves, is the dearer resource).  The store goes
 // through a buffer resource whose range is the sequence, so lanes past it
 // are dropped by the range check: no exec mask, no 64-bit address per lane.
-__device__ __forceinline__ void store_short_seq(uint8_t* out, int pos, uint32_t total, uint32_t a, uint32_t lit,
-                                                uint32_t lb, uint32_t tok, uint32_t remL, uint32_t remM,
-                                                uint32_t off) {
+// da = lane - a; tok: the token, in a VGPR (token_v).
+__device__ __forceinline__ void store_short_seq(__amdgpu_buffer_rsrc_t out_rsrc, int pos, uint32_t total, uint32_t da, uint32_t b,
+                                                uint32_t lit, uint32_t lb, uint32_t tok, uint32_t remL,
+                                                uint32_t remM, uint32_t off) {
   const uint32_t lane = lane_id();
-  const uint32_t b = a + lit;
   uint32_t hv = 255u;
-  hv = writelane(remL, a - 1u, hv);
-  hv = writelane(tok, 0u, hv);
   hv = writelane(remM, total - 1u, hv);
-  hv = writelane(off & 255u, b, hv);
-  hv = writelane(off >> 8, b + 1u, hv);
-  const uint32_t val = lane - a < lit ? lb : hv;
-  // the range ends at the sequence's last byte: pos + total bytes from out
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(out, 0, pos + (int)total, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val, r, pos + (int)lane, 0, 0);
+  hv = writelane(remL, 1u, hv);
+  hv = lane == 0u ? tok : hv;
+  const uint32_t d = lane - b;                      // the offset's bytes: d = 0, 1
+  hv = d < 2u ? off >> (d << 3) : hv;               // (a byte store keeps bits 7:0)
+  const uint32_t val = da < lit ? lb : hv;
+  // lanes past the sequence's last byte get an offset past the resource's
+  // range (out_rsrc), which the range check drops
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val, out_rsrc, lane < total ? pos + (int)lane : (int)0x80000000, 0, 0);
+}
+
+// The token (lz4.cc:535-550, 580-592), min(lit, 15) << 4 | min(ml, 15), made
+// on the vector unit from the scalar lengths (three VALU instead of four SALU:
+// the CU's one scalar unit is the dearer resource here).
+__device__ __forceinline__ uint32_t token_v(uint32_t lit, uint32_t ml) {
+  uint32_t a, b, t;
+  asm("v_min_u32_e64 %0, %1, 15" : "=v"(a) : "s"(lit));
+  asm("v_min_u32_e64 %0, %1, 15" : "=v"(b) : "s"(ml));
+  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(t) : "v"(a), "v"(b));
+  return t;
 }
 
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
@@ -363,75 +377,39 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // its start is known (at the end of the sequence before), so the read
     // overlaps that sequence's byte store
     typename Src::Word seq0 = src.rd32_issue(clamp4(s + lane));
-    // One sequence per call: 0 = a match was encoded (on to the next unless
-    // it ended past mflimit), 1 = no match (to the last literals), 2 =
-    // limitedOutput failure.  kLead: the search starts with a lead chunk
-    // (every sequence but a value's first), so its lane masks are constants.
-    auto sequence = [&](auto lead_c) -> int {
-      constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
-      src.step(s);
-      // ================= search (lz4.cc:494-527), 64 iterations per step
-      // (the loop exits with the chunk that matched; a chunk that runs past
-      // mflimit without a match goes to the last literals)
-      uint32_t pk, refk;
-      typename Tab::Slot slot;
-      uint64_t mm, vm;
-      // the lead chunk's lane masks, per sequence (t0 != 0: lane 0 put only,
-      // lane 1 dead, lane 2 valid unconditionally -- see above)
-      const uint64_t lead_or = t0 ? 5ull : 0ull, lead_and = t0 ? ~2ull : ~0ull;
-      const uint64_t lead_mm = t0 ? ~1ull : ~0ull, lead_full = t0 ? 2ull : 0ull;
-      const uint32_t o3 = 3u * t0;
-      // First chunk (nearly every sequence's only one): step(k) = 1 for k <= 64,
-      // so its positions are s-o3+lane.
-      {
-        pk = s - o3 + lane;
-        // valid lanes (lz4.cc:510), as a compare straight into a lane mask
-        // pk + 1 <= mflimit as a compare of the lane index with a scalar
-        // bound (no pk in the chain: s <= mflimit + 1, so it is >= -2)
-        vm = (__builtin_amdgcn_sicmp((int)lane, (int)(mflimit - 1u - s + o3), 41 /*SLE*/) | lead_or) & lead_and;
-        const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
-        const uint32_t seq = Src::word(seq0);
-        const uint32_t h = hashp<kWide>(seq);
-        // get + put of every valid lane at once, in lane order: refk is the
-        // entry as the sequential loop's get at this iteration reads it
-        refk = tab.xchg(h, pk, valid, slot);
-        // the lanes whose reference matches (lz4.cc:527, 610-616), as a
-        // compare straight into a lane mask (a ballot of a bool would be
-        // materialised in a VGPR and compared again); byU32 adds the
-        // distance check (lz4.cc:526, 614), byU16 sizes never need it.
-        // refk is a position <= mflimit of this value (the table holds
-        // nothing else), so its 4 bytes need no clamp.
-        mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) & vm & lead_mm;
-        if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
-      }
-      // later chunks: no match yet and every lane valid (else: last literals)
-      if (__builtin_expect((mm | ~(vm | lead_full)) == 0, 0)) {
-        uint32_t kb = 0;
-#pragma unroll 1
-        for (;;) {
-          kb += 64u;
-          // k >= 61: the closed form with no k == 0 case
-          const uint32_t k = kb + lane - o3;
-          pk = search_pos_nz<kWide>(s, k);
-          vm = __builtin_amdgcn_uicmp(pk + ((63u + k) >> 6), mflimit, 37 /*ULE*/);
-          const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);
-          const uint32_t seq = RD32(clamp4(pk));
-          const uint32_t h = hashp<kWide>(seq);
-          refk = tab.xchg(h, pk, valid, slot);
-          mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) & vm;
-          if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
-          if ((mm | ~vm) != 0) break;                // a match, or past mflimit
-        }
-      }
-      if (__builtin_expect(!mm, 0)) return 1;
+    // One sequence per call.  The sequence loop runs while anchor < lim_end:
+    // mflimit + 1 (lz4.cc:597: a match that ends past mflimit leaves for the
+    // last literals), or 0 once a search finds no match (the last literals)
+    // or limitedOutput fails (guard_fail) -- a bound, not a status word, so
+    // the loop's test is one scalar compare and no flag is carried.  kLead:
+    // the search starts with a lead chunk (every sequence but a value's
+    // first), so its lane masks are constants.
+    uint32_t lim_end = mflimit + 1u;
+    bool guard_fail = false;
+    // the block's bytes, as a buffer resource whose range (2^31 - 1 bytes)
+    // only the "past the sequence" offset 2^31 leaves
+    const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+    // the lead chunk's compare keys (see the search below): lane 0 and 2
+    // always valid, lane 1 never; for a match lanes 0 and 1 never
+    const int key_put = lane == 1u ? INT32_MAX : (lane == 0u || lane == 2u) ? INT32_MIN : (int)lane;
+    const int key_match = lane <= 1u ? INT32_MAX : lane == 2u ? INT32_MIN : (int)lane;
+    // The rest of a sequence once its search found a match (mm: the matching
+    // lanes, pk/refk/slot: the chunk's positions, entries and table slots).
+    auto finish = [&](uint64_t mm, uint32_t pk, uint32_t refk, const typename Tab::Slot& slot) {
       const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
       uint32_t ip = readlane(pk, ks);
       uint32_t ref = readlane(refk, ks);
       // undo the puts of the lanes after ks (the sequential loop stops at ks):
       // per slot, the lowest such lane holds the entry as lanes <= ks left it
       // -- its refk is a position <= ip (positions grow with the lane; entries
-      // from before the chunk are smaller still)
-      if (__builtin_amdgcn_inverse_ballot_w64(vm & ~mask_le(ks)) && refk <= ip) tab.restore(slot, refk);
+      // from before the chunk are smaller still).  The lanes after ks are the
+      // ones with pk > ip, and every lane's refk < pk, so the test is
+      // refk <= ip < pk, one unsigned compare: (ip - refk) < (pk - refk).
+      // Lanes whose exchange was off (invalid, dead) pass it too: one that
+      // read an entry <= ip writes back what the slot holds as of ks (a later
+      // lane that overwrote it restores the same entry), and its nibble mask
+      // is 0.
+      if (ip - refk < pk - refk) tab.restore(slot, refk);
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml, ip_end;
@@ -443,14 +421,25 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // the reads go out first (lanes past lim / rem read something
         // harmless, clamped into the value only in HBM); the masks are
         // built while they are in flight
-        const uint32_t a0 = src.u8(clamp1(ip - 1u - lane)), b0 = src.u8(clamp1(ref - 1u - lane));
-        const uint32_t a1 = src.u8(clamp1(ip + kMinMatch + lane));
+        const uint32_t ia = ip - 1u - lane, ra = ref - 1u - lane, ib = ip + kMinMatch + lane;
+        const uint32_t a0 = src.u8(clamp1(ia)), b0 = src.u8(clamp1(ra));
+        const uint32_t a1 = src.u8(clamp1(ib));
         const uint32_t b1 = src.u8(clamp1(ref + kMinMatch + lane));
-        const uint64_t clm = __builtin_amdgcn_uicmp(lane, lim, 36 /*ULT*/);   // lanes < lim
-        const uint64_t mlm = __builtin_amdgcn_uicmp(lane, rem, 36 /*ULT*/);   // lanes < rem
-        // compares straight into lane masks; lanes past lim / rem vote false
-        const int c0 = first_zero_or_neg(__builtin_amdgcn_uicmp(a0, b0, 32 /*EQ*/) & clm);
-        const int ml0 = first_zero_or_neg(__builtin_amdgcn_uicmp(a1, b1, 32 /*EQ*/) & mlm);
+        // compares straight into lane masks; lanes past lim / rem vote false:
+        // their byte is replaced by 256, which no byte equals.  lane < lim is
+        // ia >= anchor and ra >= 0, lane < rem is ib < matchlimit: compares of
+        // the read addresses on the vector unit, selects rather than an AND of
+        // masks on the CU's one scalar unit (the 256 is opaque so the compiler
+        // does not fold the selects back into one)
+        uint32_t k256 = 256u;
+        asm volatile("" : "+v"(k256));
+        // (in-place values, whose reads are clamped, compare the lane with
+        // lim and rem: measured a little faster there)
+        const uint32_t x0 = kFree ? ((int)ra >= 0 ? ((int)ia >= (int)anchor ? a0 : k256) : k256)
+                                  : (lane < lim ? a0 : k256);
+        const uint32_t x1 = kFree ? (ib < matchlimit ? a1 : k256) : (lane < rem ? a1 : k256);
+        const int c0 = first_zero_or_neg(__builtin_amdgcn_uicmp(x0, b0, 32 /*EQ*/));
+        const int ml0 = first_zero_or_neg(__builtin_amdgcn_uicmp(x1, b1, 32 /*EQ*/));
         c = (uint32_t)c0;
         ml = (uint32_t)ml0;
         if (__builtin_expect(ml0 < 0, 0)) {
@@ -493,20 +482,25 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // encoding is at most its input + lit/255 bytes, so op stays below
         // anchor + anchor/255 and both sides stay under the bound's 16 spare
         // bytes); the unguarded instantiation omits them.
-        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap) return 2;
         const int op_off = op + 1 + (lit >= kRunMask ? (int)((lit - kRunMask) / 255u) + 1 : 0) + (int)lit;
-        if (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap) return 2;
+        if (op + 1 + (int)lit + (int)(2 + 1 + kLastLiterals) + (int)(lit / 255u) > cap ||
+            (long_ml && op_off + 2 + (int)(1 + kLastLiterals) + (int)(ml >> 8) > cap)) {
+          guard_fail = true;
+          lim_end = 0;
+          return;
+        }
       }
       const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
-      uint32_t nl1, nm1, remL, remM;                 // remL/remM < 255 each
+      uint32_t nl1, nm1, remL, remM;   // remL/remM: the run's last byte in bits 7:0
       // at most one run byte each (almost every sequence): (n+241)>>8 is
-      // (n >= 15), the byte n-15; without a run its "last byte" index falls
-      // on a byte of higher precedence, so any 8-bit value does.  Longer runs
-      // override (an if without an else: one scalar branch, no flags)
-      nl1 = (lit + 241u) >> 8;
-      nm1 = (ml + 241u) >> 8;
-      remL = (lit - 15u) & 255u;
-      remM = (ml - 15u) & 255u;
+      // (n >= 15), the byte n-15 = bits 7:0 of n+241 (the byte stores keep
+      // bits 7:0, so no mask); without a run its "last byte" index falls on a
+      // byte of higher precedence, so any value does.  Longer runs override
+      // (an if without an else: one scalar branch, no flags)
+      remL = lit + 241u;
+      remM = ml + 241u;
+      nl1 = remL >> 8;
+      nm1 = remM >> 8;
       if (__builtin_expect(max(lit, ml) >= 270u, 0)) {
         nl1 = run_bytes(lit);
         nm1 = run_bytes(ml);
@@ -523,29 +517,97 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // whose literal read shares their round trip (measured a little faster
       // than issuing them right after the match length)
       seq0 = src.rd32_issue(clamp4(s - 3u + lane));
-      // a sequence of <= 64 bytes in one store (its range 0 -- nothing stored
-      // -- for a longer one, which emit_seq writes): no if/else around it
+      // a sequence of <= 64 bytes in one store, no if/else around it: a
+      // longer one (rare) stores its first 64 bytes here too, some of them
+      // wrong, and emit_seq then rewrites all of its bytes -- each lane's
+      // later store to the same address lands after its earlier one
       if (!kGuard) {
-        const uint32_t lb = src.u8(clamp1(seq_anchor - ea + lane));
-        store_short_seq(out, seq_op, etot <= 64u ? etot : 0u, ea, lit, lb, token, remL, remM, moff);
+        const uint32_t da = lane - ea;                // lane's literal index
+        const uint32_t lb = src.u8(clamp1(seq_anchor + da));
+        store_short_seq(out_rsrc, seq_op, etot, da, ea + lit, lit, lb, token_v(lit, ml), remL, remM, moff);
       }
       if (kGuard || __builtin_expect(etot > 64u, 0))
         emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, seq_anchor, true, moff, nm1, remM);
-      return 0;
     };
-    int st = sequence(std::false_type{});
+    auto sequence = [&](auto lead_c) {
+      constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
+      src.step(s);
+      // ================= search (lz4.cc:494-527), 64 iterations per step
+      // (the loop exits with the chunk that matched; a chunk that runs past
+      // mflimit without a match goes to the last literals)
+      uint32_t pk, refk;
+      typename Tab::Slot slot;
+      uint64_t mm, vm;
+      const uint32_t o3 = 3u * t0;
+      // First chunk (nearly every sequence's only one): step(k) = 1 for k <= 64,
+      // so its positions are s-o3+lane.
+      // valid lanes (lz4.cc:510): pk + 1 <= mflimit, a compare of the lane
+      // index with a scalar bound (no pk in the chain: s <= mflimit + 1, so
+      // it is >= -2).  A lead chunk's lanes 0 and 2 are valid whatever the
+      // bound (lane 0 puts, lane 2 tests), lane 1 never (dead), and only
+      // lanes >= 2 may match: their compare keys (key_put, key_match) make
+      // each mask one vector compare, with no scalar mask arithmetic.
+      const int bound = (int)(mflimit - 1u - s + o3);
+      {
+        pk = s - o3 + lane;
+        vm = __builtin_amdgcn_sicmp(t0 ? key_put : (int)lane, bound, 41 /*SLE*/);
+        const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
+        const uint32_t seq = Src::word(seq0);
+        const uint32_t h = hashp<kWide>(seq);
+        // get + put of every valid lane at once, in lane order: refk is the
+        // entry as the sequential loop's get at this iteration reads it
+        refk = tab.xchg(h, pk, valid, slot);
+        // the lanes whose reference matches (lz4.cc:527, 610-616), as a
+        // compare straight into a lane mask (a ballot of a bool would be
+        // materialised in a VGPR and compared again); byU32 adds the
+        // distance check (lz4.cc:526, 614), byU16 sizes never need it.
+        // refk is a position <= mflimit of this value (the table holds
+        // nothing else), so its 4 bytes need no clamp.
+        mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) &
+             (t0 ? __builtin_amdgcn_sicmp(key_match, bound, 41 /*SLE*/) : vm);
+        if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
+      }
+      // later chunks: no match yet and every lane valid, i.e. lane 63 (else:
+      // last literals); the two tests nested, so the common path is one
+      // scalar compare and branch
+      if (__builtin_expect(mm == 0, 0)) {
+       if (bound >= 63) {
+        uint32_t kb = 0;
+#pragma unroll 1
+        for (;;) {
+          kb += 64u;
+          // k >= 61: the closed form with no k == 0 case
+          const uint32_t k = kb + lane - o3;
+          pk = search_pos_nz<kWide>(s, k);
+          vm = __builtin_amdgcn_uicmp(pk + ((63u + k) >> 6), mflimit, 37 /*ULE*/);
+          const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);
+          const uint32_t seq = RD32(clamp4(pk));
+          const uint32_t h = hashp<kWide>(seq);
+          refk = tab.xchg(h, pk, valid, slot);
+          mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) & vm;
+          if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
+          if ((mm | ~vm) != 0) break;                // a match, or past mflimit
+        }
+       }
+       if (!mm) {
+         lim_end = 0;
+         return;
+       }
+       // a later chunk matched: the sequence's rest, a copy of its own (were
+       // the paths to join, the compiler would carry a flag across the join)
+       finish(mm, pk, refk, slot);
+       return;
+      }
+      finish(mm, pk, refk, slot);
+    };
+    sequence(std::false_type{});
     // lz4.cc:597 (the match ended past mflimit: the last literals); else the
     // table fill of ip-2 (lz4.cc:600) and the test of ip run as the next
     // (lead) chunk, positions ip-2+lane (seq0 above).  The test is made here,
     // at the branch, so no flag carries it across the sequence's byte store.
-    if (st == 0) {
 #pragma unroll 1
-      while (anchor <= mflimit) {
-        st = sequence(std::true_type{});
-        if (__builtin_expect(st != 0, 0)) break;
-      }
-    }
-    if (kGuard && st == 2) return 0;
+    while (anchor < lim_end) sequence(std::true_type{});
+    if (kGuard && guard_fail) return 0;
   }
 
   {  // the last literals (lz4.cc:625-637)
