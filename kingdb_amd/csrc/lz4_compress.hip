@@ -297,45 +297,10 @@ __device__ __forceinline__ int emit_seq(uint8_t* __restrict__ out, int out_cap, 
   return (int)total;
 }
 
-// A sequence of at most 64 encoded bytes (nearly all) in one byte store per
-// lane, byte j of the encoding on lane j: token at 0, the literal-length
-// run's last byte at a-1 (a = 1 + nl1, nl1 <= 1 here), literals [a, a+lit)
-// (lb: this lane's literal byte), offset at b, b+1 (b = a+lit), the
-// match-length run's last byte at total-1, 255 elsewhere.  The token, remL
-// and remM go in with v_writelane (remL always at lane 1: with no run, lane 1
-// is a literal or the offset's low byte, which take precedence), the offset's
-// two bytes are shifted out of the offset by each lane's distance from b, so
-// a lane's byte is two selects and only remM's lane goes through m0 (each
-// writelane at a variable lane costs a scalar m0 write: the CU's one scalar
-// unit, shared by its waves, is the dearer resource).  The store goes
-// through a buffer resource whose range is the sequence, so lanes past it
-// are dropped by the range check: no exec mask, no 64-bit address per lane.
-// da = lane - a; tok: the token, in a VGPR (token_v).
-__device__ __forceinline__ void store_short_seq(__amdgpu_buffer_rsrc_t out_rsrc, int pos, uint32_t total, uint32_t da, uint32_t b,
-                                                uint32_t lit, uint32_t lb, uint32_t tok, uint32_t remL,
-                                                uint32_t remM, uint32_t off) {
-  const uint32_t lane = lane_id();
-  uint32_t hv = 255u;
-  hv = writelane(remM, total - 1u, hv);
-  hv = writelane(remL, 1u, hv);
-  hv = lane == 0u ? tok : hv;
-  const uint32_t d = lane - b;                      // the offset's bytes: d = 0, 1
-  hv = d < 2u ? off >> (d << 3) : hv;               // (a byte store keeps bits 7:0)
-  const uint32_t val = da < lit ? lb : hv;
-  // lanes past the sequence's last byte get an offset past the resource's
-  // range (out_rsrc), which the range check drops
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val, out_rsrc, lane < total ? pos + (int)lane : (int)0x80000000, 0, 0);
-}
-
-// The token (lz4.cc:535-550, 580-592), min(lit, 15) << 4 | min(ml, 15), made
-// on the vector unit from the scalar lengths (three VALU instead of four SALU:
-// the CU's one scalar unit is the dearer resource here).
-__device__ __forceinline__ uint32_t token_v(uint32_t lit, uint32_t ml) {
-  uint32_t a, b, t;
-  asm("v_min_u32_e64 %0, %1, 15" : "=v"(a) : "s"(lit));
-  asm("v_min_u32_e64 %0, %1, 15" : "=v"(b) : "s"(ml));
-  asm("v_lshl_or_b32 %0, %1, 4, %2" : "=v"(t) : "v"(a), "v"(b));
-  return t;
+// x in a VGPR (every lane the same value): arithmetic on it is VALU
+__device__ __forceinline__ uint32_t vgpr_u32(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
 }
 
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
@@ -372,11 +337,11 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // lane 2 = ip, the test, valid unconditionally (ip <= mflimit was
     // checked); lanes >= 3 = search iterations 0..60.  A lane-2 match is
     // _next_match: no catch-up, no literals.
-    uint32_t s = 1;                                         // lz4.cc:487
+    // the search starts at anchor + 1 (lz4.cc:487, 623): no variable of its own
     // the input words of the next sequence's first chunk, read as soon as
     // its start is known (at the end of the sequence before), so the read
     // overlaps that sequence's byte store
-    typename Src::Word seq0 = src.rd32_issue(clamp4(s + lane));
+    typename Src::Word seq0 = src.rd32_issue(clamp4(1u + lane));
     // One sequence per call.  The sequence loop runs while anchor < lim_end:
     // mflimit + 1 (lz4.cc:597: a match that ends past mflimit leaves for the
     // last literals), or 0 once a search finds no match (the last literals)
@@ -386,6 +351,11 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // first), so its lane masks are constants.
     uint32_t lim_end = mflimit + 1u;
     bool guard_fail = false;
+    // the search's lane bound mflimit - 1 - s + o3 (s = anchor + 1) is
+    // kbound - anchor: one scalar subtract (the constants are opaque, or the
+    // compiler rebuilds it as two)
+    uint32_t kbound0 = mflimit - 2u, kbound1 = mflimit + 1u;
+    asm volatile("" : "+s"(kbound0), "+s"(kbound1));
     // the block's bytes, as a buffer resource whose range (2^31 - 1 bytes)
     // only the "past the sequence" offset 2^31 leaves
     const __amdgpu_buffer_rsrc_t out_rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
@@ -431,18 +401,20 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // the read addresses on the vector unit, selects rather than an AND of
         // masks on the CU's one scalar unit (the 256 is opaque so the compiler
         // does not fold the selects back into one)
-        uint32_t k256 = 256u;
-        asm volatile("" : "+v"(k256));
+        uint32_t k256 = 256u, k257 = 257u;           // two, so the nested selects stay two
+        asm volatile("" : "+v"(k256), "+v"(k257));
         // (in-place values, whose reads are clamped, compare the lane with
         // lim and rem: measured a little faster there)
-        const uint32_t x0 = kFree ? ((int)ra >= 0 ? ((int)ia >= (int)anchor ? a0 : k256) : k256)
+        const uint32_t x0 = kFree ? ((int)ra >= 0 ? ((int)ia >= (int)anchor ? a0 : k256) : k257)
                                   : (lane < lim ? a0 : k256);
         const uint32_t x1 = kFree ? (ib < matchlimit ? a1 : k256) : (lane < rem ? a1 : k256);
         const int c0 = first_zero_or_neg(__builtin_amdgcn_uicmp(x0, b0, 32 /*EQ*/));
         const int ml0 = first_zero_or_neg(__builtin_amdgcn_uicmp(x1, b1, 32 /*EQ*/));
         c = (uint32_t)c0;
         ml = (uint32_t)ml0;
-        if (__builtin_expect(ml0 < 0, 0)) {
+        // one scalar test for the rare continuations of either count
+        if (__builtin_expect((c0 | ml0) < 0, 0)) {
+        if (ml0 < 0) {
           ml = 64u;
 #pragma unroll 1
           for (;;) {
@@ -454,10 +426,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
             if (d < 64u) break;
           }
         }
-        // the match ends at ip_end whatever the catch-up
-        ip_end = ip + kMinMatch + ml;
-        s = ip_end + 1u;                                        // lz4.cc:623
-        if (__builtin_expect(c0 < 0, 0)) {
+        if (c0 < 0) {
           c = 64u;
 #pragma unroll 1
           for (;;) {
@@ -468,6 +437,10 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
             if (d < 64u) break;
           }
         }
+        }
+        // the match ends at ip_end whatever the catch-up; the next search
+        // starts at ip_end + 1 (lz4.cc:623), i.e. anchor + 1
+        ip_end = ip + kMinMatch + ml;
       }
       ip -= c;
       ref -= c;
@@ -490,48 +463,73 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           return;
         }
       }
-      const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
-      uint32_t nl1, nm1, remL, remM;   // remL/remM: the run's last byte in bits 7:0
       // at most one run byte each (almost every sequence): (n+241)>>8 is
       // (n >= 15), the byte n-15 = bits 7:0 of n+241 (the byte stores keep
       // bits 7:0, so no mask); without a run its "last byte" index falls on a
-      // byte of higher precedence, so any value does.  Longer runs override
-      // (an if without an else: one scalar branch, no flags)
-      remL = lit + 241u;
-      remM = ml + 241u;
-      nl1 = remL >> 8;
-      nm1 = remM >> 8;
-      if (__builtin_expect(max(lit, ml) >= 270u, 0)) {
-        nl1 = run_bytes(lit);
-        nm1 = run_bytes(ml);
-        remL = run_last(lit, nl1);
-        remM = run_last(ml, nm1);
-      }
-      const uint32_t ea = 1u + nl1;
-      const uint32_t etot = ea + lit + 2u + nm1;
-      const int seq_op = op;
-      const uint32_t seq_anchor = anchor;
-      op += (int)etot;
-      anchor = ip_end;
-      // the next sequence's input words go out before this sequence's bytes,
-      // whose literal read shares their round trip (measured a little faster
-      // than issuing them right after the match length)
-      seq0 = src.rd32_issue(clamp4(s - 3u + lane));
-      // a sequence of <= 64 bytes in one store, no if/else around it: a
-      // longer one (rare) stores its first 64 bytes here too, some of them
-      // wrong, and emit_seq then rewrites all of its bytes -- each lane's
-      // later store to the same address lands after its earlier one
-      if (!kGuard) {
-        const uint32_t da = lane - ea;                // lane's literal index
+      // byte of higher precedence, so any value does.  Longer runs -- lit or
+      // ml >= 270 -- take the exact run_bytes / run_last.
+      if constexpr (kGuard) {
+        const uint32_t token = (min(lit, kRunMask) << 4) | min(ml, kMlMask);
+        uint32_t nl1 = (lit + 241u) >> 8, nm1 = (ml + 241u) >> 8, remL = lit + 241u, remM = ml + 241u;
+        if (max(lit, ml) >= 270u) {
+          nl1 = run_bytes(lit);
+          nm1 = run_bytes(ml);
+          remL = run_last(lit, nl1);
+          remM = run_last(ml, nm1);
+        }
+        const int seq_op = op;
+        op += (int)(lit + nl1 + nm1 + 3u);
+        emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, anchor, true, moff, nm1, remM);
+        anchor = ip_end;
+        seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+      } else {
+        // The encoding's arithmetic on the vector unit, on uniform VGPR
+        // copies of lit and ml (the CU's one scalar unit, shared by its
+        // waves, is the dearer resource: +8 scalar instructions per sequence
+        // cost 6.9 %, +8 vector ones 2.9 %), and op lives in a VGPR too.
+        // One scalar test remains: a run of 2+ bytes or an encoding over 64
+        // bytes (rare) goes to emit_seq with the exact lengths, after the
+        // one-store path has written its first <= 64 bytes (some wrong, all
+        // rewritten: the one-store total never exceeds the exact one, and
+        // each lane's later store to the same address lands after its
+        // earlier one).
+        const uint32_t vlit = vgpr_u32(lit), vml = vgpr_u32(ml);
+        const uint32_t remL = vlit + 241u, remM = vml + 241u;
+        const uint32_t nl1 = remL >> 8, nm1 = remM >> 8;
+        const uint32_t etot = vlit + nl1 + nm1 + 3u;  // 1 + nl1 + lit + 2 + nm1
+        const int seq_op = op;
+        const uint32_t seq_anchor = anchor;
+        op = seq_op + (int)etot;
+        anchor = ip_end;
+        // the next sequence's input words go out before this sequence's
+        // bytes, whose literal read shares their round trip
+        seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+        // byte j of the encoding on lane j: token (0), remL (1 if nl1),
+        // literals [a, b) with a = 1 + nl1, b = a + lit, the offset LE16 at
+        // b, b+1, remM at b+2 (if nm1); lanes past etot are dropped
+        const uint32_t da = (lane - 1u) - nl1;        // lane - a: the lane's literal index
         const uint32_t lb = src.u8(clamp1(seq_anchor + da));
-        store_short_seq(out_rsrc, seq_op, etot, da, ea + lit, lit, lb, token_v(lit, ml), remL, remM, moff);
+        const uint32_t head = ((min(vlit, kRunMask) << 4) | min(vml, kMlMask)) | (remL << 8);
+        const uint32_t tail = moff | (remM << 16);
+        const uint32_t d = da - vlit;                 // lane - b
+        uint32_t val = lane < 2u ? head >> (lane << 3) : 255u;
+        val = d < 3u ? tail >> (d << 3) : val;
+        val = da < vlit ? lb : val;
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)val, out_rsrc, lane < etot ? seq_op + (int)lane : (int)0x80000000,
+                                             0, 0);
+        const int rare = unii((int)(510u - max(remL, remM)) | (64 - (int)etot));
+        if (__builtin_expect(rare < 0, 0)) {
+          const uint32_t xl = run_bytes(lit), xm = run_bytes(ml);
+          const int pos = unii(seq_op);
+          emit_seq<false>(out, out_cap, pos, (min(lit, kRunMask) << 4) | min(ml, kMlMask), lit, xl,
+                          run_last(lit, xl), src, S, seq_anchor, true, moff, xm, run_last(ml, xm));
+          op = pos + (int)(lit + xl + xm + 3u);
+        }
       }
-      if (kGuard || __builtin_expect(etot > 64u, 0))
-        emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, seq_anchor, true, moff, nm1, remM);
     };
     auto sequence = [&](auto lead_c) {
       constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
-      src.step(s);
+      src.step(anchor + 1u);
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
       // mflimit without a match goes to the last literals)
@@ -547,9 +545,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // bound (lane 0 puts, lane 2 tests), lane 1 never (dead), and only
       // lanes >= 2 may match: their compare keys (key_put, key_match) make
       // each mask one vector compare, with no scalar mask arithmetic.
-      const int bound = (int)(mflimit - 1u - s + o3);
+      const int bound = (int)((t0 ? kbound1 : kbound0) - anchor);
       {
-        pk = s - o3 + lane;
+        pk = anchor + 1u - o3 + lane;
         vm = __builtin_amdgcn_sicmp(t0 ? key_put : (int)lane, bound, 41 /*SLE*/);
         const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
         const uint32_t seq = Src::word(seq0);
@@ -578,7 +576,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           kb += 64u;
           // k >= 61: the closed form with no k == 0 case
           const uint32_t k = kb + lane - o3;
-          pk = search_pos_nz<kWide>(s, k);
+          pk = search_pos_nz<kWide>(anchor + 1u, k);
           vm = __builtin_amdgcn_uicmp(pk + ((63u + k) >> 6), mflimit, 37 /*ULE*/);
           const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);
           const uint32_t seq = RD32(clamp4(pk));
@@ -618,7 +616,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
                            false, 0u, 0u, 0u);
   }
 #undef RD32
-  return op;
+  return unii(op);
 }
 
 constexpr uint32_t kSmallMax = 4096u;     // tagged table + register prefetch
