@@ -129,51 +129,61 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // results are scalar already -- and only the literal half and the
       // positions stay on the VALU: 3.60 -> 3.56 ms at 1 Mi x 4 KiB (the whole
       // sequence on the scalar unit measured 4.44, the header too 3.87).
-      int vip = vgpr(ip), vop = vgpr(op);
-      uint32_t vq = vgpr(q);
+      // Positions are kept as per-lane absolute LDS addresses (lane i: the
+      // byte at position + i), so the literal store, the match read and the
+      // match store need no address add; the bounds are per-lane constants
+      // shifted the same way, and lane 0 (readfirstlane) sees the plain
+      // differences.  The token's fields come out of its SGPR with v_bfe.
+      typedef __attribute__((address_space(3))) uint8_t lds_b;
+      const uint32_t in_abs = lds_addr(lds_in) + in_off;
+      const int ob = (int)lds_addr(out);
+      const int obl = vgpr(ob + (int)lane), ibl = vgpr((int)in_abs + (int)lane);
+      const int oexit_l = oexit + obl, oend5_l = oend5 + obl, iend8_l = iend8 + ibl;
+      int avip = ibl + ip, aop = obl + op;
       uint32_t sq = q;                     // the token word in an SGPR
-      // a sequence's literal-run header from its token word tq at tip: lx (a
-      // literal-length byte follows), xl (its value or 0), lit, ls (first literal)
-      int lx, xl, lit, ls;
-      auto header = [&](uint32_t tq, int tip) {
-        const int ln = (int)(tq & 0xffu) >> 4, b1 = (int)((tq >> 8) & 0xffu);
+      // a sequence's literal-run header from its token word tq (SGPR) at
+      // als-address atip: lx (a literal-length byte follows), xl (its value
+      // or 0), lit, als (the first literal's per-lane address)
+      int lx, xl, lit, als;
+      auto header = [&](uint32_t tq, int atip) {
+        int ln, b1;
+        asm("v_bfe_u32 %0, %1, 4, 4" : "=v"(ln) : "s"(tq));
+        asm("v_bfe_u32 %0, %1, 8, 8" : "=v"(b1) : "s"(tq));
         lx = (ln + 1) >> 4;
         xl = b1 & -lx;
         lit = ln + xl;                                            // <= 60 iff !lx || b1 <= 45
-        ls = tip + 1 + lx;
+        als = atip + 1 + lx;
       };
-      header(vq, vip);
+      header(sq, avip);
       // lane i holds the block's 4 bytes from ls + i: byte 0 is literal i,
       // and one readlane gives the offset + match-length byte, another the
       // next token and the byte after it.  The load goes out before the
       // fast-path test (its address is inside the staged block plus the
       // window slack for any token; a sequence that fails the test never
       // uses it), so both tests are one scalar decision.
-      const uint32_t in_abs = lds_addr(lds_in) + in_off;
-      uint32_t v = lds_rd32_at(in_abs + (uint32_t)(ls + (int)lane));
+      uint32_t v = lds_rd32_at((uint32_t)als);
 #pragma unroll 1
       for (;;) {
         const int mn = (int)(sq & 0xffu) & (int)kMlMask;
         const int slit = unii(lit);
-        const int opl = vop + lit;
+        const int aopl = aop + lit;
         const uint32_t w = readlane(v, (uint32_t)slit & 63u);   // offset, match-length byte
         const int e = (int)((w >> 16) & 0xffu);
         const int off = (int)(w & 0xffffu);
         const int mx = (mn + 1) >> 4;                             // a match-length byte follows
         const int xm = e & -mx;
         const int mlen = mn + xm + (int)kMinMatch;
+        const int aref = aopl - off;
         // far from both ends, <= 60 literals, ref >= 0, one match-length byte
-        if ((unii((iend8 - ls - lit) | (oexit - opl) | (45 - xl) | (opl - off) | ((oend5 - mlen) - opl)) |
+        if ((unii((iend8_l - als - lit) | (oexit_l - aopl) | (45 - xl) | (aref - obl) | ((oend5_l - mlen) - aopl)) |
              (254 - xm)) < 0)
           break;
-        out[vop + (int)lane] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
+        ((lds_b*)(uintptr_t)(uint32_t)aop)[0] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
         const int nt = slit + 2 + mx;                             // next token's lane (<= 63)
         sq = readlane(v, (uint32_t)nt);
-        vq = vgpr(sq);
-        vip = ls + nt;
-        header(vq, vip);
-        v = lds_rd32_at(in_abs + (uint32_t)(ls + (int)lane));   // the next sequence's literals
-        const int ref = opl - off;
+        avip = als + nt;
+        header(sq, avip);
+        v = lds_rd32_at((uint32_t)als);                           // the next sequence's literals
         asm volatile("" ::: "memory");
         // the match's first 64-byte step as a plain copy, unconditionally
         // (mlen >= 4; lanes past mlen write the not-yet-produced tail); only
@@ -181,11 +191,12 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         // 0) or one longer than a step takes the branch, which for an
         // overlapping match rewrites the whole match (a plain copy may have
         // read bytes of this step before they were written)
-        const uint8_t b0 = out[ref + (int)lane];
-        out[opl + (int)lane] = b0;
+        const uint8_t b0 = ((const lds_b*)(uintptr_t)(uint32_t)aref)[0];
+        ((lds_b*)(uintptr_t)(uint32_t)aopl)[0] = b0;
         asm volatile("" ::: "memory");
         if (((off - min(mlen, 64)) | (64 - mlen)) < 0) {
           const int steps = unii(mlen);
+          const int opl = unii(aopl) - ob, ref = opl - off;
           if (off - min(mlen, 64) < 0) {
             if (off > 0) {                        // periodic (see the general path)
               const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
@@ -209,11 +220,11 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
           }
         }
         asm volatile("" ::: "memory");
-        vop = opl + mlen;
+        aop = aopl + mlen;
       }
-      ip = unii(vip);
-      op = unii(vop);
-      q = (uint32_t)unii((int)vq);
+      ip = unii(avip) - (int)in_abs;
+      op = unii(aop) - ob;
+      q = sq;
     }
     const uint32_t token = q & 0xffu;
     ip++;
