@@ -201,27 +201,21 @@ struct LdsSrc {
   __device__ __forceinline__ void step(uint32_t) {}
 };
 
-// Value bytes read in place from global memory (any alignment).  An aligned
-// dword never lies on a page no needed byte lies on, so the reads cannot fault.
+// Value bytes read in place from global memory (any alignment).
 struct GlobalSrc {
   static constexpr bool kUnclamped = false;
   const uint8_t* g;
   uint32_t S;
   uint32_t keep;   // the frontier touch in flight (see step)
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return g[i]; }
-  __device__ __forceinline__ uint32_t rd32(uint32_t i) const {
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3u);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(g + i - mis);
-    return __builtin_amdgcn_alignbyte(w[mis ? 1 : 0], w[0], mis);
-  }
-  // rd32 in two halves: the loads (issued early), then the realignment
-  struct Word { uint32_t lo, hi, sh; };
-  __device__ __forceinline__ Word rd32_issue(uint32_t i) const {
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3u);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(g + i - mis);
-    return Word{w[0], w[mis ? 1 : 0], mis};
-  }
-  __device__ __forceinline__ static uint32_t word(const Word& w) { return __builtin_amdgcn_alignbyte(w.hi, w.lo, w.sh); }
+  // one unaligned dword load (gfx950's global loads take any alignment): every
+  // caller's 4 bytes lie inside the value (positions <= mflimit, or clamped
+  // to S - 4), so the load never touches a page past it
+  typedef uint32_t __attribute__((aligned(1))) u32u;
+  __device__ __forceinline__ uint32_t rd32(uint32_t i) const { return *reinterpret_cast<const u32u*>(g + i); }
+  struct Word { uint32_t v; };
+  __device__ __forceinline__ Word rd32_issue(uint32_t i) const { return Word{rd32(i)}; }
+  __device__ __forceinline__ static uint32_t word(const Word& w) { return w.v; }
   // Touches the 256 bytes from p + 256 (one aligned dword per lane, clamped
   // into the value) so the search frontier is in L1/L2 before it is parsed;
   // the previous touch's dword is consumed here -- one sequence later, when
