@@ -533,7 +533,11 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     };
     auto sequence = [&](auto lead_c) {
       constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
-      src.step(anchor + 1u);
+      // the frontier touch (GlobalSrc::step) only for byU32 values: for the
+      // byU16 in-place class its load, issued ahead of the search's reads,
+      // cost more than it saved (64 KiB 6.51 -> 6.36 ms without it; 1 MiB
+      // byU32 9.84 -> 10.71 ms without it, profiles/r02_e40_ab_touch.txt)
+      if constexpr (kWide) src.step(anchor + 1u);
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
       // mflimit without a match goes to the last literals)
