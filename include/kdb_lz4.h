@@ -36,8 +36,21 @@ int kdb_lz4_version(void); /* 10000*major + 100*minor + patch */
 
 /* ---------------------------------------------------------------- runtime */
 int kdb_lz4_device_count(int* count);
+/* Binds `device` for the calling thread and runs its lane-order self-test
+ * (kdb_lz4_selftest) if it has not run yet. */
 int kdb_lz4_set_device(int device);
 int kdb_lz4_get_device(int* device);
+/* The compressor's exactness rests on one LDS behaviour: the lanes of one
+ * ds_mskor_rtn_b32 that hit the same dword apply in ascending lane order
+ * (lz4_compress.hip, the exchange tables).  This runs the device self-test of
+ * that behaviour once per device (later calls return the cached verdict):
+ * *state = 1 passed, -1 failed (then every compress entry point returns
+ * KDB_LZ4_EUNSUPPORTED on that device, never a frame), 0 not run;
+ * *bad_lanes (optional) = mismatching lane results seen. */
+int kdb_lz4_selftest(int device, int* state, uint32_t* bad_lanes);
+/* The kernels (rocprof names, ';'-separated) that the calling thread's last
+ * compress or decompress batch queued.  No HIP call. */
+int kdb_lz4_last_kernels(char* buf, uint64_t cap);
 int kdb_lz4_malloc(void** ptr, uint64_t bytes);              /* device memory */
 int kdb_lz4_free(void* ptr);
 int kdb_lz4_host_alloc(void** ptr, uint64_t bytes);          /* pinned host memory */

@@ -19,11 +19,15 @@ from .lz4 import (  # noqa: F401
     decompress_safe_partial,
     device_count,
     frame_bound,
+    get_device,
+    last_kernels,
+    selftest,
     set_device,
 )
 
 __all__ = [
     "DeviceBatch", "DeviceBuffer", "Event", "Stream", "compress_blocks", "compress_bound",
     "compress_frames", "compress_limited_output", "decompress_blocks", "decompress_frames",
-    "decompress_safe_partial", "device_count", "frame_bound", "set_device",
+    "decompress_safe_partial", "device_count", "frame_bound", "get_device", "last_kernels", "selftest",
+    "set_device",
 ]

@@ -230,6 +230,14 @@ struct BatchStaging {
     host = dev = stream = nullptr;
     cap = 0;
   }
+  // After a failed call: wait for whatever the stream still has queued; if
+  // even that fails, forget the buffers (leaked, not freed: a kernel may still
+  // write them) so the next call allocates fresh ones.
+  void drain_or_drop() {
+    if (stream && kdb_lz4_stream_sync(stream) == KDB_LZ4_OK) return;
+    host = dev = stream = nullptr;
+    cap = 0;
+  }
   bool reserve(uint64_t bytes) {
     int d = 0;
     if (kdb_lz4_get_device(&d) != KDB_LZ4_OK) return false;
@@ -299,7 +307,10 @@ Status CompressorLZ4::CompressFrames(uint32_t n, char* const* raw_in, const uint
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb, db, meta, st);
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb + meta + src_bytes, db + meta + src_bytes, dst_bytes, st);
   if (!rc) rc = kdb_lz4_stream_sync(st);
-  if (rc) return Status::IOError("GPU compress batch failed");
+  if (rc) {
+    b.drain_or_drop();   // nothing queued may still write the staging the next call reuses
+    return Status::IOError("GPU compress batch failed");
+  }
   for (uint32_t i = 0; i < n; i++) {
     if (status[i] != 0) {
       for (uint32_t j = 0; j < i; j++) {
@@ -361,7 +372,10 @@ Status CompressorLZ4::UncompressFrames(uint32_t n, char* const* frames, const ui
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb, db, meta, st);
   if (!rc) rc = kdb_lz4_memcpy_d2h(hb + meta + src_bytes, db + meta + src_bytes, dst_bytes, st);
   if (!rc) rc = kdb_lz4_stream_sync(st);
-  if (rc) return Status::IOError("GPU decompress batch failed");
+  if (rc) {
+    b.drain_or_drop();
+    return Status::IOError("GPU decompress batch failed");
+  }
   for (uint32_t i = 0; i < n; i++) {
     if (status[i] != 0) return Status::IOError("LZ4_decompress_safe_partial() failed", std::to_string(i));
     memcpy(out[i], hb + dst_off[i], out_len[i]);

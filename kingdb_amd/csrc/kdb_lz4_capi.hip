@@ -35,6 +35,7 @@ inline int hip_status(hipError_t e) {
   if (e == hipSuccess) return KDB_LZ4_OK;
   if (e == hipErrorNoDevice || e == hipErrorInvalidDevice || e == hipErrorInsufficientDriver)
     return KDB_LZ4_ENODEV;
+  if (e == hipErrorNotSupported) return KDB_LZ4_EUNSUPPORTED;   // the lane-order self-test failed
   return KDB_LZ4_EHIP;
 }
 
@@ -62,6 +63,17 @@ struct ScalarCtx {
     if (dev) (void)hipFree(dev);
     if (host) (void)hipHostFree(host);
     if (stream) (void)hipStreamDestroy(stream);
+  }
+  // A failed call returns only once nothing it queued can still write the
+  // staging the next call reuses; if the stream cannot even be drained, the
+  // buffers are dropped (leaked, not freed) and the next call allocates anew.
+  int failed(int ret) {
+    if (stream && hipStreamSynchronize(stream) != hipSuccess) {
+      host = hdev = dev = nullptr;
+      hcap = dcap = 0;
+      stream = nullptr;
+    }
+    return ret;
   }
   static size_t grow(size_t have, size_t bytes) {
     size_t want = have ? have : 1u << 16;
@@ -134,7 +146,35 @@ int kdb_lz4_device_count(int* count) {
   *count = e == hipSuccess ? n : 0;
   return e == hipSuccess ? KDB_LZ4_OK : KDB_LZ4_ENODEV;
 }
-int kdb_lz4_set_device(int device) { return hip_status(hipSetDevice(device)); }
+// Binding a device runs its lane-order self-test (selftest.hip) at once, so a
+// device the compressor cannot be exact on is reported here, not mid-batch.
+int kdb_lz4_set_device(int device) {
+  const int rc = hip_status(hipSetDevice(device));
+  if (rc != KDB_LZ4_OK) return rc;
+  const hipError_t e = lane_order_check();
+  return e == hipErrorNotSupported ? KDB_LZ4_OK : hip_status(e);   // the failure shows at compress time
+}
+int kdb_lz4_selftest(int device, int* state, uint32_t* bad_lanes) {
+  if (!state) return KDB_LZ4_EINVAL;
+  int cur = 0;
+  hipError_t e = hipGetDevice(&cur);
+  if (e != hipSuccess) return hip_status(e);
+  if (device != cur && (e = hipSetDevice(device)) != hipSuccess) return hip_status(e);
+  e = lane_order_check();
+  const int rc = e == hipSuccess || e == hipErrorNotSupported ? KDB_LZ4_OK : hip_status(e);
+  *state = lane_order_state(device, bad_lanes);
+  if (device != cur) (void)hipSetDevice(cur);
+  return rc;
+}
+int kdb_lz4_last_kernels(char* buf, uint64_t cap) {
+  if (!buf || cap == 0) return KDB_LZ4_EINVAL;
+  const char* s = launch_notes();
+  const size_t n = strlen(s);
+  const size_t k = n < cap - 1 ? n : (size_t)cap - 1;
+  memcpy(buf, s, k);
+  buf[k] = 0;
+  return KDB_LZ4_OK;
+}
 int kdb_lz4_get_device(int* device) { return device ? hip_status(hipGetDevice(device)) : KDB_LZ4_EINVAL; }
 int kdb_lz4_malloc(void** ptr, uint64_t bytes) {
   return ptr ? hip_status(hipMalloc(ptr, bytes ? bytes : 1)) : KDB_LZ4_EINVAL;
@@ -203,7 +243,7 @@ int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize
     if (launch_compress(false, c.stream, c.hdev, &dm->src_off, &dm->len, 1, S, S, c.hdev, &dm->dst_off, &dm->cap,
                         nullptr, &dm->ret) != hipSuccess ||
         hipStreamSynchronize(c.stream) != hipSuccess)
-      return 0;
+      return c.failed(0);
     m = read_meta(c.host);
     if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
     return m.ret > 0 ? m.ret : 0;
@@ -223,7 +263,7 @@ int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize
                       nullptr, &dm->ret) != hipSuccess ||
       hipMemcpyAsync(c.host, c.dev, in_at, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
       hipStreamSynchronize(c.stream) != hipSuccess)
-    return 0;
+    return c.failed(0);
   m = read_meta(c.host);
   if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
   return m.ret > 0 ? m.ret : 0;
@@ -254,7 +294,7 @@ int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compress
     if (launch_decompress(false, c.stream, c.hdev, &dm->src_off, &dm->len, 1, C, O, c.hdev, &dm->dst_off, &dm->cap,
                           &dm->target, &dm->out_len, &dm->ret) != hipSuccess ||
         hipStreamSynchronize(c.stream) != hipSuccess)
-      return -1;
+      return c.failed(-1);
     m = read_meta(c.host);
     if (m.ret == KDB_LZ4_VALUE_UNSUPPORTED) return -1;
     if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);
@@ -274,7 +314,7 @@ int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compress
                         &dm->target, &dm->out_len, &dm->ret) != hipSuccess ||
       hipMemcpyAsync(c.host, c.dev, in_at, hipMemcpyDeviceToHost, c.stream) != hipSuccess ||
       hipStreamSynchronize(c.stream) != hipSuccess)
-    return -1;
+    return c.failed(-1);
   m = read_meta(c.host);
   if (m.ret == KDB_LZ4_VALUE_UNSUPPORTED) return -1;
   if (m.ret > 0) memcpy(dest, c.host + out_at, (size_t)m.ret);

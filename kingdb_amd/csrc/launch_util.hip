@@ -6,8 +6,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <cstring>
 #include <mutex>
-#include <functional>
 #include <unordered_map>
 
 namespace kdb_lz4 {
@@ -132,23 +132,58 @@ uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
 // (the last few big values) no longer idles the rest of the GPU.  One
 // non-blocking stream and two events per host thread, device and CALLER
 // stream: batches a caller issues on different streams keep their own aux
-// streams, so one batch's big class never queues behind another's.
+// streams, so one batch's big class never queues behind another's.  The set
+// is bounded per thread (kForks, least recently used out): a caller that
+// makes a stream per request does not grow it without end; an evicted aux
+// stream is drained before it is destroyed.
 namespace {
 struct Fork {
+  int dev = -1;
+  hipStream_t st = nullptr;
   hipStream_t aux = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  uint64_t used = 0;
 };
-struct ForkKey {
-  int dev;
-  hipStream_t st;
-  bool operator==(const ForkKey& o) const { return dev == o.dev && st == o.st; }
-};
-struct ForkKeyHash {
-  size_t operator()(const ForkKey& k) const {
-    return std::hash<const void*>()(k.st) ^ (std::hash<int>()(k.dev) * 0x9e3779b97f4a7c15ull);
+constexpr int kForks = 8;
+thread_local Fork t_fork[kForks];
+thread_local uint64_t t_fork_clock = 0;
+
+void fork_destroy(Fork& f) {
+  if (f.aux) {
+    (void)hipStreamSynchronize(f.aux);
+    (void)hipStreamDestroy(f.aux);
   }
-};
-thread_local std::unordered_map<ForkKey, Fork, ForkKeyHash> t_fork;
+  if (f.fork) (void)hipEventDestroy(f.fork);
+  if (f.join) (void)hipEventDestroy(f.join);
+  f = Fork();
+}
+
+// the entry of (dev, st); with create, a fresh one in the least recently used slot
+Fork* fork_of(int dev, hipStream_t st, bool create, hipError_t* e) {
+  *e = hipSuccess;
+  Fork* lru = &t_fork[0];
+  for (Fork& f : t_fork) {
+    if (f.aux && f.dev == dev && f.st == st) {
+      f.used = ++t_fork_clock;
+      return &f;
+    }
+    if (f.used < lru->used) lru = &f;
+  }
+  if (!create) return nullptr;
+  fork_destroy(*lru);
+  Fork f;
+  f.dev = dev;
+  f.st = st;
+  if ((*e = hipStreamCreateWithFlags(&f.aux, hipStreamNonBlocking)) != hipSuccess ||
+      (*e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming)) != hipSuccess ||
+      (*e = hipEventCreateWithFlags(&f.join, hipEventDisableTiming)) != hipSuccess) {
+    fork_destroy(f);
+    return nullptr;
+  }
+  f.used = ++t_fork_clock;
+  *lru = f;
+  return lru;
+}
 }  // namespace
 
 hipError_t fork_begin(hipStream_t st, hipStream_t* aux) {
@@ -158,15 +193,11 @@ hipError_t fork_begin(hipStream_t st, hipStream_t* aux) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  Fork& f = t_fork[ForkKey{dev, st}];
-  if (!f.aux) {
-    if ((e = hipStreamCreateWithFlags(&f.aux, hipStreamNonBlocking)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&f.fork, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventCreateWithFlags(&f.join, hipEventDisableTiming)) != hipSuccess) return e;
-  }
-  if ((e = hipEventRecord(f.fork, st)) != hipSuccess) return e;
-  if ((e = hipStreamWaitEvent(f.aux, f.fork, 0)) != hipSuccess) return e;
-  *aux = f.aux;
+  Fork* f = fork_of(dev, st, true, &e);
+  if (!f) return e;
+  if ((e = hipEventRecord(f->fork, st)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(f->aux, f->fork, 0)) != hipSuccess) return e;
+  *aux = f->aux;
   return hipSuccess;
 }
 
@@ -176,9 +207,10 @@ hipError_t fork_end(hipStream_t st, hipStream_t aux) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  Fork& f = t_fork[ForkKey{dev, st}];
-  if ((e = hipEventRecord(f.join, aux)) != hipSuccess) return e;
-  return hipStreamWaitEvent(st, f.join, 0);
+  Fork* f = fork_of(dev, st, false, &e);
+  if (!f || f->aux != aux) return hipErrorInvalidHandle;
+  if ((e = hipEventRecord(f->join, aux)) != hipSuccess) return e;
+  return hipStreamWaitEvent(st, f->join, 0);
 }
 
 // Ranges per launch.  Tiny values saturate one counter (128 Ki 100-byte
@@ -202,5 +234,25 @@ uint32_t claim_batch(uint32_t n, uint32_t grid) {
 }
 
 uint32_t env_prio() { return kdb_tune("KDB_LZ4_BIGPRIO", 0) != 0 ? 1u : 0u; }
+
+namespace {
+thread_local char t_notes[512];
+thread_local size_t t_notes_len = 0;
+}  // namespace
+
+void launch_notes_reset() {
+  t_notes_len = 0;
+  t_notes[0] = 0;
+}
+
+void launch_note(const char* kernel) {
+  const size_t k = strlen(kernel);
+  if (t_notes_len + k + 2 > sizeof(t_notes)) return;
+  if (t_notes_len) t_notes[t_notes_len++] = ';';
+  memcpy(t_notes + t_notes_len, kernel, k + 1);
+  t_notes_len += k;
+}
+
+const char* launch_notes() { return t_notes; }
 
 }  // namespace kdb_lz4

@@ -937,11 +937,13 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = claim_batch(n, grid);
+  launch_note(F ? (Sm ? "lz4_compress_kernel<true, true>" : "lz4_compress_kernel<true, false>")
+                : (Sm ? "lz4_compress_kernel<false, true>" : "lz4_compress_kernel<false, false>"));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap));
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return work_counter_release(st, work);
+  const hipError_t r = work_counter_release(st, work);   // the slot is fenced even when the launch failed
+  return e != hipSuccess ? e : r;
 }
 
 template <bool F, bool W>
@@ -956,11 +958,13 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
+  launch_note(F ? (W ? "lz4_compress_big_kernel<true, true>" : "lz4_compress_big_kernel<true, false>")
+                : (W ? "lz4_compress_big_kernel<false, true>" : "lz4_compress_big_kernel<false, false>"));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, prio);
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return work_counter_release(st, work);
+  const hipError_t r = work_counter_release(st, work);
+  return e != hipSuccess ? e : r;
 }
 
 template <bool F>
@@ -972,13 +976,15 @@ static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_
   uint32_t *wb = nullptr, *ws = nullptr;
   hipError_t e = launch_counter(st, n, grid, &wb);
   if (e == hipSuccess) e = launch_counter(st, n, grid, &ws);
-  if (e != hipSuccess) return e;
-  const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, big_min, big_max, dst, dst_off,
-                     dst_cap, frame_len, ret, wb, bb, ws, bs, work_queues(kSmallMax));
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = work_counter_release(st, wb)) != hipSuccess) return e;
-  return work_counter_release(st, ws);
+  if (e == hipSuccess) {
+    const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
+    launch_note(F ? "lz4_compress_mixed_kernel<true>" : "lz4_compress_mixed_kernel<false>");
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, big_min, big_max, dst, dst_off,
+                       dst_cap, frame_len, ret, wb, bb, ws, bs, work_queues(kSmallMax));
+    e = hipGetLastError();
+  }
+  const hipError_t r1 = work_counter_release(st, wb), r2 = work_counter_release(st, ws);
+  return e != hipSuccess ? e : r1 != hipSuccess ? r1 : r2;
 }
 
 // One launch per size class that [min_len, max_len] (the launch's bounds on
@@ -991,9 +997,13 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
                            const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst,
                            const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                            int32_t* ret) {
+  launch_notes_reset();
   if (n == 0) return hipSuccess;
   if (min_len > max_len) min_len = 0;
-  hipError_t e;
+  // the exchange tables' lane order, verified on this device before its first
+  // frame (selftest.hip); a device without it compresses nothing
+  hipError_t e = lane_order_ok();
+  if (e != hipSuccess) return e;
   static const uint32_t mid_split = (uint32_t)kdb_tune("KDB_LZ4_CSPLIT", kMidLdsMax);
   const uint32_t b1 = min(max(mid_split, kSmallMax), k64KLimit - 1u);   // top of the LDS-staged class
   // class c covers lengths [lo[c], hi[c]]
@@ -1020,51 +1030,58 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   const bool combo = on[0] && on[2];
   hipStream_t aux = st;
   const bool fork = combo ? on[3] : ((on[2] || on[3]) && (on[0] || on[1]));
-  if (fork) {
-    e = fork_begin(st, &aux);
-    if (e != hipSuccess) return e;
-  }
-  if (combo) {
-    e = frame ? launch_mixed<true>(st, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len, ret)
-              : launch_mixed<false>(st, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len, ret);
-    if (e != hipSuccess) return e;
-  }
-  if (on[2] && !combo) {
-    e = frame ? launch_big<true, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
-                                        ret, census, 2)
-              : launch_big<false, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
-                                         ret, census, 2);
-    if (e != hipSuccess) return e;
-  }
-  if (on[3]) {
-    e = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
-                                       frame_len, ret, census, 3)
-              : launch_big<false, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
-                                        frame_len, ret, census, 3);
-    if (e != hipSuccess) return e;
-  }
-  if (on[0] && !combo) {
-    const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
-    e = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                       frame_len, ret, census, 0)
-              : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                        frame_len, ret, census, 0);
-    if (e != hipSuccess) return e;
-  }
-  // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
-  // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
-  // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
-  if (on[1]) {
-    const uint32_t top = min(max_len, hi[1]);
-    const size_t lds = compress_lds_bytes(top);
-    e = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
-                                        dst_cap, frame_len, ret, census, 1)
-              : launch_one<false, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
-                                         dst_cap, frame_len, ret, census, 1);
-    if (e != hipSuccess) return e;
-  }
-  if (fork && (e = fork_end(st, aux)) != hipSuccess) return e;
-  return work_counter_release(st, census);   // its readers are all joined into st by now
+  // The class launches stop at the first error, but the join of the forked
+  // stream and the census slot's fence always follow: a caller that reuses
+  // its buffers after an error must not race a kernel still queued on aux.
+  auto classes_run = [&]() -> hipError_t {
+    hipError_t r = hipSuccess;
+    if (combo) {
+      r = frame ? launch_mixed<true>(st, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len, ret)
+                : launch_mixed<false>(st, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len, ret);
+      if (r != hipSuccess) return r;
+    }
+    if (on[2] && !combo) {
+      r = frame ? launch_big<true, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap, frame_len,
+                                          ret, census, 2)
+                : launch_big<false, false>(aux, src, src_off, src_len, n, lo[2], hi[2], dst, dst_off, dst_cap,
+                                           frame_len, ret, census, 2);
+      if (r != hipSuccess) return r;
+    }
+    if (on[3]) {
+      r = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
+                                         frame_len, ret, census, 3)
+                : launch_big<false, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
+                                          frame_len, ret, census, 3);
+      if (r != hipSuccess) return r;
+    }
+    if (on[0] && !combo) {
+      const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
+      r = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                         frame_len, ret, census, 0)
+                : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
+                                          frame_len, ret, census, 0);
+      if (r != hipSuccess) return r;
+    }
+    // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
+    // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
+    // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
+    if (on[1]) {
+      const uint32_t top = min(max_len, hi[1]);
+      const size_t lds = compress_lds_bytes(top);
+      r = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
+                                          dst_cap, frame_len, ret, census, 1)
+                : launch_one<false, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
+                                           dst_cap, frame_len, ret, census, 1);
+    }
+    return r;
+  };
+  e = fork ? fork_begin(st, &aux) : hipSuccess;
+  if (e == hipSuccess) e = classes_run();
+  const hipError_t j = fork ? fork_end(st, aux) : hipSuccess;          // aux == st when fork_begin failed
+  const hipError_t c = work_counter_release(st, census);                // its readers are all joined into st
+  if (e == hipSuccess) e = j;
+  if (e == hipSuccess) e = c;
+  return e;
 }
 
 }  // namespace kdb_lz4

@@ -22,6 +22,7 @@
 // suffices (the same bytes as the reference's dec32/dec64 copy, lz4.cc:1008-1018).
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "lz4_device.h"
 
@@ -930,11 +931,12 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = claim_batch(n, grid);
+  launch_note(F ? "lz4_decompress_kernel<true>" : "lz4_decompress_kernel<false>");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
                      out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out));
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return work_counter_release(st, work);
+  const hipError_t r = work_counter_release(st, work);   // the slot is fenced even when the launch failed
+  return e != hipSuccess ? e : r;
 }
 
 template <bool F, uint32_t R>
@@ -949,11 +951,14 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
+  static const std::string name = std::string(F ? "lz4_decompress_big_kernel<true, " : "lz4_decompress_big_kernel<false, ") +
+                                  std::to_string(R) + "u>";
+  launch_note(name.c_str());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
                      dst_off, out_cap, target, out_len, ret, work, batch, prio);
   e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return work_counter_release(st, work);
+  const hipError_t r = work_counter_release(st, work);
+  return e != hipSuccess ? e : r;
 }
 
 
@@ -992,13 +997,15 @@ static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_
   uint32_t *wb = nullptr, *ws = nullptr;
   hipError_t e = launch_counter(st, n, grid, &wb);
   if (e == hipSuccess) e = launch_counter(st, n, grid, &ws);
-  if (e != hipSuccess) return e;
-  const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst, dst_off,
-                     out_cap, target, out_len, ret, wb, bb, ws, bs, work_queues(out_small));
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = work_counter_release(st, wb)) != hipSuccess) return e;
-  return work_counter_release(st, ws);
+  if (e == hipSuccess) {
+    const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
+    launch_note(F ? "lz4_decompress_mixed_kernel<true>" : "lz4_decompress_mixed_kernel<false>");
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
+                       dst_off, out_cap, target, out_len, ret, wb, bb, ws, bs, work_queues(out_small));
+    e = hipGetLastError();
+  }
+  const hipError_t r1 = work_counter_release(st, wb), r2 = work_counter_release(st, ws);
+  return e != hipSuccess ? e : r1 != hipSuccess ? r1 : r2;
 }
 
 // LDS-resident decoder for outputs up to 65 546 bytes (blocks up to the bound
@@ -1012,6 +1019,7 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,
                              uint8_t* dst, const uint64_t* dst_off, const uint32_t* out_cap,
                              const uint32_t* target, uint32_t* out_len, int32_t* ret) {
+  launch_notes_reset();
   if (n == 0) return hipSuccess;
   // LDS-resident decoder up to `split` output bytes, the ring decoder above
   static const uint32_t split = min((uint32_t)kdb_tune("KDB_LZ4_DSPLIT", 8192), kOutSmallMax);
@@ -1037,19 +1045,24 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                  : launch_mixed<false>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target, out_len,
                                        ret);
   }
+  if (ring_only)
+    return frame ? launch_ring<true>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
+                 : launch_ring<false>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len,
+                                      ret);
+  // the join always follows once the fork began, whatever failed after it: a
+  // caller that reuses its buffers after an error must not race the aux stream
   if (big) {
-    if (!ring_only && (e = fork_begin(st, &aux)) != hipSuccess) return e;
+    if ((e = fork_begin(st, &aux)) != hipSuccess) return e;
     e = frame ? launch_ring<true>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
               : launch_ring<false>(aux, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret);
-    if (e != hipSuccess) return e;
-    if (ring_only) return hipSuccess;
   }
-  e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
-                               out_len, ret, big ? 1u : 0u)
-            : launch_one<false>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
-                                out_len, ret, big ? 1u : 0u);
-  if (e != hipSuccess) return e;
-  return fork_end(st, aux);
+  if (e == hipSuccess)
+    e = frame ? launch_one<true>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
+                                 out_len, ret, big ? 1u : 0u)
+              : launch_one<false>(st, lds, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target,
+                                  out_len, ret, big ? 1u : 0u);
+  const hipError_t j = fork_end(st, aux);
+  return e != hipSuccess ? e : j;
 }
 
 }  // namespace kdb_lz4

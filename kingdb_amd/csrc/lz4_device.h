@@ -207,5 +207,25 @@ hipError_t fork_end(hipStream_t st, hipStream_t aux);
 // wave priority of the big-value (in-place / ring) class launches, whose
 // values are a mixed batch's critical path (KDB_LZ4_BIGPRIO, default 0)
 uint32_t env_prio();
+// The kernels the calling thread's last launch_compress / launch_decompress
+// queued, by their rocprof names (kdb_lz4_last_kernels): the bench labels its
+// roofline with them instead of guessing from the size classes.
+// The compressor's lane-order guard (selftest.hip): runs the device self-test
+// once per device; hipErrorNotSupported when the device fails it.
+hipError_t lane_order_check();
+int lane_order_state(int dev, uint32_t* bad);
+// lane_order_check behind a per-thread cache of the last device that passed
+inline hipError_t lane_order_ok() {
+  static thread_local int ok_dev = -1;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess || dev == ok_dev) return e;
+  e = lane_order_check();
+  if (e == hipSuccess) ok_dev = dev;
+  return e;
+}
+void launch_notes_reset();
+void launch_note(const char* kernel);
+const char* launch_notes();
 
 }  // namespace kdb_lz4

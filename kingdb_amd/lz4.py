@@ -43,6 +43,27 @@ def set_device(dev: int) -> None:
     _lib.check(lib().kdb_lz4_set_device(dev), "set_device")
 
 
+def get_device() -> int:
+    d = ctypes.c_int(-1)
+    _lib.check(lib().kdb_lz4_get_device(ctypes.byref(d)), "get_device")
+    return d.value
+
+
+def selftest(dev: int) -> tuple:
+    """(state, bad_lanes) of the device's lane-order self-test (kdb_lz4_selftest):
+    state 1 passed, -1 failed, 0 not run."""
+    st, bad = ctypes.c_int(0), ctypes.c_uint32(0)
+    _lib.check(lib().kdb_lz4_selftest(dev, ctypes.byref(st), ctypes.byref(bad)), "selftest")
+    return st.value, bad.value
+
+
+def last_kernels() -> list:
+    """Kernels (rocprof names) the calling thread's last compress/decompress batch queued."""
+    buf = ctypes.create_string_buffer(1024)
+    _lib.check(lib().kdb_lz4_last_kernels(buf, len(buf)), "last_kernels")
+    return [k for k in buf.value.decode().split(";") if k]
+
+
 # ------------------------------------------------------------ device memory
 class DeviceBuffer:
     """A hipMalloc'd byte range owned by Python."""

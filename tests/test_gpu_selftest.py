@@ -1,0 +1,67 @@
+"""GPU: the compressor's lane-order guard (kingdb_amd/csrc/selftest.hip).
+
+The exchange tables of lz4_compress.hip rest on one LDS behaviour (the lanes
+of one ds_mskor_rtn_b32 that hit the same dword apply in ascending lane
+order).  Every device the library binds runs a self-test of it first:
+* kdb_lz4_set_device runs it, and it passes on MI355X;
+* a device that fails it compresses nothing -- every compress entry point
+  returns KDB_LZ4_EUNSUPPORTED (the scalar mirror: 0), never a frame
+  (KDB_LZ4_SELFTEST_FORCE_FAIL=1 drives that path in a child process);
+* decompression does not depend on it and keeps working.
+Also: the library names the kernels a batch queued (kdb_lz4_last_kernels),
+which bench.py uses for its roofline label.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_selftest_ran_and_passed(gpu):
+    import kingdb_amd as K
+    K.set_device(0)
+    state, bad = K.selftest(0)
+    assert state == 1 and bad == 0
+    assert K.get_device() == 0
+
+
+def test_selftest_failure_blocks_compression():
+    code = r'''
+import sys
+sys.path.insert(0, %r)
+import kingdb_amd as K
+from kingdb_amd import _lib
+K.set_device(0)
+state, bad = K.selftest(0)
+assert state == -1 and bad >= 1, (state, bad)
+try:
+    K.compress_frames([b"abc" * 100])
+    raise SystemExit("compress_frames returned frames on a failed device")
+except RuntimeError as e:
+    assert str(_lib.EUNSUPPORTED) in str(e) or "EUNSUPPORTED" in str(e), e
+assert K.compress_limited_output(b"abc" * 100, 400) == (0, b"")
+frame = bytes([0, 0, 0, 0, 3, 0, 0, 0]) + b"xyz"          # a raw-fallback frame decodes without the table
+st, out = K.decompress_frames([frame], [3])[0]
+assert st == 0 and out == b"xyz", (st, out)
+print("ok")
+''' % ROOT
+    env = dict(os.environ, KDB_LZ4_SELFTEST_FORCE_FAIL="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_last_kernels_names(gpu):
+    import kingdb_amd as K
+    K.compress_frames([b"x" * 4096] * 4)
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true>"]
+    K.compress_frames([b"x" * 6000] * 4)
+    assert K.last_kernels() == ["lz4_compress_kernel<true, false>"]
+    K.compress_frames([b"x" * 4096, b"y" * 20000])
+    assert K.last_kernels() == ["lz4_compress_mixed_kernel<true>"]
+    K.compress_frames([b"x" * 100000])
+    assert K.last_kernels() == ["lz4_compress_big_kernel<true, true>"]
