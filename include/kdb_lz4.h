@@ -48,6 +48,11 @@ int kdb_lz4_get_device(int* device);
  * KDB_LZ4_EUNSUPPORTED on that device, never a frame), 0 not run;
  * *bad_lanes (optional) = mismatching lane results seen. */
 int kdb_lz4_selftest(int device, int* state, uint32_t* bad_lanes);
+/* Readies the current device for the first real call: runs its lane-order
+ * self-test and one small batch through every kernel family (so the code
+ * object is loaded and the runtime's first-launch costs are paid here, not
+ * inside a caller's timed or latency-critical path).  Synchronous; idempotent. */
+int kdb_lz4_warmup(void);
 /* The kernels (rocprof names, ';'-separated) that the calling thread's last
  * compress or decompress batch queued.  No HIP call. */
 int kdb_lz4_last_kernels(char* buf, uint64_t cap);

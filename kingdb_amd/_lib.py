@@ -33,6 +33,7 @@ SIGNATURES = {
     "kdb_lz4_get_device": (_i, [_c.POINTER(_i)]),
     "kdb_lz4_selftest": (_i, [_i, _c.POINTER(_i), _c.POINTER(_u32)]),
     "kdb_lz4_last_kernels": (_i, [_c.c_char_p, _u64]),
+    "kdb_lz4_warmup": (_i, []),
     "kdb_lz4_malloc": (_i, [_c.POINTER(_vp), _u64]),
     "kdb_lz4_free": (_i, [_vp]),
     "kdb_lz4_host_alloc": (_i, [_c.POINTER(_vp), _u64]),
@@ -60,6 +61,9 @@ SIGNATURES = {
     "kdb_lz4_decompress_frames_batch": (_i, [_vp, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _vp]),
     "kdb_lz4_pack_frames": (_i, [_vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     "kdb_lz4_gen_g1": (_i, [_vp, _u64, _u64, _u32, _vp]),
+    # include/kdb_flush.h (the write-buffer flush batch)
+    "kdb_flush_scratch_bytes": (_u64, [_u32, _u32, _u64]),
+    "kdb_flush_parts_batch": (_i, [_vp] * 12 + [_u32, _u32, _u32, _u32, _vp, _u64, _u64, _vp, _vp, _vp, _vp]),
     # include/kdb_put.h (the write path around the codec)
     "kdb_put_scratch_bytes": (_u64, [_u32, _u32, _u64]),
     "kdb_put_entries_batch": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _vp, _u64,

@@ -11,6 +11,7 @@
 #include "compressor.h"
 
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "kdb_lz4.h"
@@ -68,6 +69,11 @@ void CRC32LZ4::stream(const char* data, size_t n) {  // crc32c.h:87-92
 }
 
 // compressor.cc:9-12
+void CompressorLZ4::WarmUp() {
+  static std::once_flag once;
+  std::call_once(once, [] { (void)kdb_lz4_warmup(); });   // no device: the calls report it later
+}
+
 void CompressorLZ4::ResetThreadLocalStorage() {
   ts_compress_.reset();
   ts_uncompress_.reset();

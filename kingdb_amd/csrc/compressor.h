@@ -67,7 +67,10 @@ uint32_t Crc32cExtend(uint32_t crc, const char* data, size_t n);
 
 class CompressorLZ4 {
  public:
-  CompressorLZ4() {}
+  // The first instance in a process readies the GPU (kdb_lz4_warmup: the
+  // lane-order self-test, the code object, the runtime's first-launch costs),
+  // so a Database pays them when it is built, not in its first puts.
+  CompressorLZ4() { WarmUp(); }
   // compressor.h:110-113: assignment does not copy state.
   CompressorLZ4& operator=(const CompressorLZ4&) { return *this; }
   virtual ~CompressorLZ4() {}
@@ -121,6 +124,7 @@ class CompressorLZ4 {
   ThreadStorageLZ4 ts_uncompress_;
   CRC32LZ4 crc32_;
   bool crc_double_stream_ = true;
+  static void WarmUp();
 };
 
 KDB_LZ4_NS_CLOSE  // namespace kdb

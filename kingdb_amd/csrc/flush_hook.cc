@@ -1,57 +1,62 @@
-// kingdb_amd/csrc/flush_hook.cc -- LZ4FlushOrders (kingdb_include/cache/lz4_flush.h):
-// the deferred single-part puts of one write-buffer flush, completed in one
-// kdb_put_entries_batch call.  Compiled by the KingDB build that applies the
-// hook (oracle/kingdb_hook.py, INTEGRATION.md level 4), like compressor.cc.
+// kingdb_amd/csrc/flush_hook.cc -- the write-buffer flush hook
+// (kingdb_include/cache/lz4_flush.h).  Compiled by the
+// KingDB build that applies the hook (oracle/kingdb_hook.py, INTEGRATION.md
+// level 4), like compressor.cc.
 //
-// For a single-part value PutPartValidSize (/root/reference/interface/database.cc:128-276)
-// queues chunk_final = the CompressorLZ4 frame, or the all-zero 8-byte header +
-// raw bytes when the disable rule (:196-209) fires; size_value_compressed =
-// |chunk_final| (:237-248); crc32 = CRC32C(key || chunk_final) (:251-257).
-// kdb_put_entries_batch computes the same three things on the GPU for the
-// whole batch (put.hip, put_policy_kernel) and returns the self-contained
-// HSTable entry EntryHeader || key || chunk_final, so chunk_final is the
-// entry's tail and its length is the entry's length minus the key and the
-// header (EntryHeader::EncodeTo, /root/reference/storage/format.h:224-255,
-// for a full single-part entry: flags kEntryFull, no padding).
+// One pipeline per write buffer:
+//   client threads   LZ4FlushDefer: the PutPartValidSize call goes into the
+//                    intake (key, chunk, offsets, thread id) under a ticket
+//   worker thread    takes the intake in ticket order, in batches (at most
+//                    kBatchBytes / kBatchParts, or whatever came within
+//                    kBatchAge, or everything when a flush asks), and runs each
+//                    batch through kdb_flush_parts_batch (include/kdb_flush.h):
+//                    frames, the disable rule, offsets, size_value_compressed
+//                    and the running CRC32C on the GPU, each client thread's
+//                    state (the reference's ThreadStorage slots,
+//                    /root/reference/interface/database.cc:159-257) carried
+//                    from batch to batch; the results wait per ticket
+//   flush thread     LZ4FlushOrders: waits for the tickets of the buffer being
+//                    flushed (usually long done: the worker runs while the
+//                    buffer fills), then completes each order in place
+// A GPU batch that fails is retried once on a fresh stream and fresh staging;
+// if that fails too its orders are dropped (never written without their frame
+// and checksum), the failure is latched and every later LZ4FlushDefer returns
+// IOError: the process keeps running.
 #include "cache/lz4_flush.h"
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
 
+#include "../../include/kdb_flush.h"
 #include "../../include/kdb_lz4.h"
-#include "../../include/kdb_put.h"
 #include "util/logger.h"
 
 namespace kdb {
 
 namespace {
 
-inline uint64_t a256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
-inline uint32_t varint_len(uint64_t v) {
-  uint32_t n = 1;
-  while (v >= 128) {
-    v >>= 7;
-    n++;
-  }
-  return n;
-}
-// EntryHeader::EncodeTo's length for a self-contained entry with compression
-// on (put.hip header_len with flags kEntryFull = 0x8 and padding 0):
-// crc8, checksum_content, flags, size_key, size_value, size_value_compressed,
-// size_padding, hash.
-inline uint64_t self_contained_header_len(uint64_t klen, uint64_t size_value) {
-  return 1 + 4 + varint_len(0x8) + varint_len(klen) + varint_len(size_value) + 8 + varint_len(0) + 8;
-}
+constexpr uint64_t kBatchBytes = 8ull << 20;   // raw bytes that start a batch at once
+constexpr size_t kBatchParts = 65536;           // parts that start a batch at once
+constexpr auto kBatchAge = std::chrono::microseconds(1000);   // oldest waiting part
 
-// Pinned host + device staging kept across flushes (one writer thread).
-struct FlushStaging {
+inline uint64_t a256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+// Pinned host + device staging of one pipeline, kept across batches.
+struct Staging {
   void* host = nullptr;
   void* dev = nullptr;
   void* stream = nullptr;
   uint64_t hcap = 0, dcap = 0;
-  int device = -1;
-  ~FlushStaging() { release(); }
+  ~Staging() { release(); }
   void release() {
     if (host) kdb_lz4_host_free(host);
     if (dev) kdb_lz4_free(dev);
@@ -59,32 +64,36 @@ struct FlushStaging {
     host = dev = stream = nullptr;
     hcap = dcap = 0;
   }
+  // after a failure: drain what the stream still has queued, or forget the
+  // buffers (leaked, not freed: a kernel may still write them)
+  void drop() {
+    if (stream && kdb_lz4_stream_sync(stream) == KDB_LZ4_OK) {
+      release();
+      return;
+    }
+    host = dev = stream = nullptr;
+    hcap = dcap = 0;
+  }
   static uint64_t grow(uint64_t cap, uint64_t want) {
-    uint64_t c = cap ? cap : (4ull << 20);
+    uint64_t c = cap ? cap : (16ull << 20);
     while (c < want) c *= 2;
     return c;
   }
   bool reserve(uint64_t hbytes, uint64_t dbytes) {
-    int d = 0;
-    if (kdb_lz4_get_device(&d) != KDB_LZ4_OK) return false;
-    if (d != device) {
-      release();
-      device = d;
-    }
     if (!stream && kdb_lz4_stream_create(&stream) != KDB_LZ4_OK) return false;
     if (hbytes > hcap) {
       if (host) kdb_lz4_host_free(host);
       host = nullptr;
-      hcap = 0;
       const uint64_t c = grow(hcap, hbytes);
+      hcap = 0;
       if (kdb_lz4_host_alloc(&host, c) != KDB_LZ4_OK) return false;
       hcap = c;
     }
     if (dbytes > dcap) {
       if (dev) kdb_lz4_free(dev);
       dev = nullptr;
-      dcap = 0;
       const uint64_t c = grow(dcap, dbytes);
+      dcap = 0;
       if (kdb_lz4_malloc(&dev, c) != KDB_LZ4_OK) return false;
       dcap = c;
     }
@@ -92,116 +101,469 @@ struct FlushStaging {
   }
 };
 
-[[noreturn]] void fatal(const std::string& what) {
-  log::emerg("LZ4FlushOrders()", "%s", what.c_str());
-  fprintf(stderr, "LZ4FlushOrders(): %s\n", what.c_str());
-  std::abort();
+struct Intake {
+  std::thread::id tid;
+  ByteArray key, chunk;
+  uint64_t offset_chunk, size_value;
+};
+
+struct Result {
+  ByteArray chunk_final;   // KDB_FLUSH_FRAME / KDB_FLUSH_DISABLED
+  uint64_t occ = 0, svc = 0;
+  uint32_t crc = 0;
+  uint8_t mode = KDB_FLUSH_RAW;
+  int8_t status = 0;       // -1: the order is dropped
+  bool consumed = false;
+};
+
+// KDB_LZ4_FLUSH_INJECT=<first>:<count> -- test knob: GPU batch attempts
+// first .. first+count-1 (counted from 1) fail as a failed
+// kdb_flush_parts_batch would (tests/test_kingdb_dropin.py).
+struct Inject {
+  uint64_t first = 0, count = 0;
+  Inject() {
+    const char* e = getenv("KDB_LZ4_FLUSH_INJECT");
+    if (!e || !*e) return;
+    char* end = nullptr;
+    first = strtoull(e, &end, 10);
+    count = end && *end == ':' ? strtoull(end + 1, nullptr, 10) : 1;
+  }
+  bool fails(uint64_t attempt) const { return first && attempt >= first && attempt - first < count; }
+};
+
+class Pipeline {
+ public:
+  explicit Pipeline(int device) : device_(device) { worker_ = std::thread(&Pipeline::run, this); }
+  ~Pipeline() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_work_.notify_all();
+    worker_.join();
+  }
+
+  Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket) {
+    bool kick;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      if (failed_) return Status::IOError("LZ4 flush pipeline failed", failure_);
+      *ticket = (uint32_t)next_ticket_++;
+      if (intake_.empty()) intake_since_ = std::chrono::steady_clock::now();
+      intake_.push_back(Intake{std::this_thread::get_id(), key, chunk, offset_chunk, size_value});
+      intake_bytes_ += chunk.size();
+      kick = intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts;
+    }
+    if (kick) cv_work_.notify_one();
+    return Status::OK();
+  }
+
+  void cancel(uint32_t ticket) {
+    std::lock_guard<std::mutex> l(res_mu_);
+    cancelled_.insert(ticket);
+  }
+
+  void complete(std::vector<Order>& orders);
+
+ private:
+  void run();
+  void process(std::vector<Intake>& batch, uint64_t t0);
+  int gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out);
+
+  // the 64-bit ticket of an order's 32 bits (outstanding tickets span < 2^32)
+  uint64_t full_ticket(uint32_t t) const { return res_base_ + (uint32_t)(t - (uint32_t)res_base_); }
+
+  const int device_;
+  std::thread worker_;
+  // intake (client threads, worker)
+  std::mutex mu_;
+  std::condition_variable cv_work_, cv_done_;
+  std::vector<Intake> intake_;
+  uint64_t intake_bytes_ = 0;
+  std::chrono::steady_clock::time_point intake_since_;
+  uint64_t next_ticket_ = 1;
+  uint64_t processed_ = 1;           // tickets below have results
+  bool drain_ = false, stop_ = false, failed_ = false;
+  std::string failure_;
+  // results (worker appends, flush thread consumes)
+  std::mutex res_mu_;
+  std::deque<Result> res_;
+  uint64_t res_base_ = 1;            // ticket of res_.front()
+  std::unordered_set<uint32_t> cancelled_;
+  // worker only
+  std::unordered_map<std::thread::id, kdb_flush_state> state_;
+  Staging stg_;
+  Inject inject_;
+  uint64_t attempts_ = 0;
+};
+
+void Pipeline::run() {
+  kdb_lz4_set_device(device_);
+  std::vector<Intake> batch;
+  for (;;) {
+    uint64_t t0;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      for (;;) {
+        if (intake_.empty()) {
+          if (drain_) {
+            drain_ = false;
+            cv_done_.notify_all();
+          }
+          if (stop_) return;
+          cv_work_.wait(lk);
+          continue;
+        }
+        if (stop_ || drain_ || intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts ||
+            std::chrono::steady_clock::now() - intake_since_ >= kBatchAge)
+          break;
+        cv_work_.wait_until(lk, intake_since_ + kBatchAge);
+      }
+      batch.swap(intake_);
+      intake_bytes_ = 0;
+      t0 = processed_;
+    }
+    process(batch, t0);   // publishes the results, then processed_
+    batch.clear();
+  }
+}
+
+void Pipeline::process(std::vector<Intake>& batch, uint64_t t0) {
+  std::vector<Result> out(batch.size());
+  int rc = gpu_batch(batch, out);
+  if (rc != KDB_LZ4_OK) {   // once more, on a fresh stream and fresh staging
+    log::emerg("LZ4FlushPipeline", "GPU batch of %zu parts failed (%d); retrying", batch.size(), rc);
+    stg_.drop();
+    rc = gpu_batch(batch, out);
+  }
+  std::string why;
+  if (rc != KDB_LZ4_OK) {
+    why = "GPU batch failed twice (" + std::to_string(rc) + ")";
+    log::emerg("LZ4FlushPipeline", "%s: %zu parts dropped", why.c_str(), batch.size());
+    stg_.drop();
+    for (Result& r : out) {
+      r = Result();
+      r.status = -1;
+    }
+  }
+  {
+    std::lock_guard<std::mutex> l(res_mu_);
+    for (Result& r : out) res_.push_back(std::move(r));
+  }
+  {
+    std::lock_guard<std::mutex> l(mu_);
+    processed_ = t0 + batch.size();
+    if (!why.empty() && !failed_) {
+      failed_ = true;
+      failure_ = why;
+    }
+  }
+  cv_done_.notify_all();
+}
+
+// The batch through the GPU: layout (segments, runs), staging, one
+// kdb_flush_parts_batch, results.  0 or a KDB_LZ4_E* code.
+int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
+  ++attempts_;
+  if (inject_.fails(attempts_)) return KDB_LZ4_EHIP;
+  const uint32_t m = (uint32_t)batch.size();
+  // ---- layout: a segment is one thread's consecutive parts of one value; a
+  // run is one thread's segments whose policy state chains (a new run starts
+  // at a first part with bytes: everything resets there, database.cc:159-179)
+  struct Cur {
+    uint32_t run, seg;
+  };
+  std::unordered_map<std::thread::id, Cur> cur;
+  std::vector<uint32_t> part_seg(m), seg_run, seg_head;   // seg_head: the segment's first entry
+  std::vector<std::thread::id> run_tid;
+  std::vector<kdb_flush_state> carry;
+  for (uint32_t i = 0; i < m; i++) {
+    const Intake& e = batch[i];
+    auto it = cur.find(e.tid);
+    const bool fresh = e.offset_chunk == 0;
+    if (it == cur.end() || (fresh && e.chunk.size_const() > 0)) {
+      const bool seen = it != cur.end();
+      const uint32_t r = (uint32_t)run_tid.size();
+      run_tid.push_back(e.tid);
+      kdb_flush_state s{};
+      if (!seen) {
+        auto st = state_.find(e.tid);
+        if (st != state_.end()) s = st->second;
+      }
+      carry.push_back(s);
+      const uint32_t sg = (uint32_t)seg_run.size();
+      seg_run.push_back(r);
+      seg_head.push_back(i);
+      if (seen) it->second = Cur{r, sg};
+      else cur.emplace(e.tid, Cur{r, sg});
+      part_seg[i] = sg;
+    } else if (fresh) {
+      const uint32_t sg = (uint32_t)seg_run.size();
+      seg_run.push_back(it->second.run);
+      seg_head.push_back(i);
+      it->second.seg = sg;
+      part_seg[i] = sg;
+    } else {
+      part_seg[i] = it->second.seg;
+    }
+  }
+  const uint32_t nseg = (uint32_t)seg_run.size(), nruns = (uint32_t)run_tid.size();
+  // order: segments grouped by run, parts grouped by segment (both stable)
+  std::vector<uint32_t> seg_order(nseg), seg_pos(nseg), run_first(nruns + 1, 0), seg_first(nseg + 1, 0),
+      perm(m);
+  const bool identity = nseg == m && nruns == m;   // every part a value of its own: nothing moves
+  if (identity) {
+    for (uint32_t i = 0; i <= m; i++) run_first[i] = seg_first[i] = i;
+    for (uint32_t i = 0; i < m; i++) perm[i] = seg_order[i] = seg_pos[i] = i;
+  } else {
+    for (uint32_t s = 0; s < nseg; s++) run_first[seg_run[s] + 1]++;
+    for (uint32_t r = 0; r < nruns; r++) run_first[r + 1] += run_first[r];
+    std::vector<uint32_t> fill(run_first.begin(), run_first.end() - 1);
+    for (uint32_t s = 0; s < nseg; s++) {
+      const uint32_t at = fill[seg_run[s]]++;
+      seg_order[at] = s;
+      seg_pos[s] = at;
+    }
+    for (uint32_t i = 0; i < m; i++) seg_first[seg_pos[part_seg[i]] + 1]++;
+    for (uint32_t s = 0; s < nseg; s++) seg_first[s + 1] += seg_first[s];
+    std::vector<uint32_t> pf(seg_first.begin(), seg_first.end() - 1);
+    for (uint32_t i = 0; i < m; i++) perm[pf[seg_pos[part_seg[i]]]++] = i;
+  }
+  // ---- staging: host [meta | keys | chunks], device [same | scratch | outputs | frames]
+  uint64_t key_bytes = 0, raw_bytes = 0, frame_cap = 0;
+  uint32_t max_chunk = 0;
+  for (uint32_t s = 0; s < nseg; s++) key_bytes += batch[seg_head[seg_order[s]]].key.size();
+  for (uint32_t i = 0; i < m; i++) {
+    const uint64_t c = batch[i].chunk.size();
+    if (c > 0x7E000000ull) return KDB_LZ4_EUNSUPPORTED;
+    raw_bytes += c;
+    frame_cap += (8 + kdb_lz4_compressBound((int)c) + 15) & ~15ull;
+    if (c > max_chunk) max_chunk = (uint32_t)c;
+  }
+  const uint64_t o_key_off = 0, o_key_len = o_key_off + a256(8ull * nseg), o_chunk_off = o_key_len + a256(4ull * nseg),
+                 o_chunk_len = o_chunk_off + a256(8ull * m), o_offset = o_chunk_len + a256(4ull * m),
+                 o_size = o_offset + a256(8ull * m), o_seg_first = o_size + a256(8ull * m),
+                 o_run_first = o_seg_first + a256(4ull * (nseg + 1)),
+                 o_carry = o_run_first + a256(4ull * (nruns + 1)),
+                 o_keys = o_carry + a256(sizeof(kdb_flush_state) * nruns), o_chunks = o_keys + a256(key_bytes),
+                 in_bytes = o_chunks + a256(raw_bytes + 64);
+  const uint64_t scratch = kdb_flush_scratch_bytes(m, nseg, raw_bytes);
+  const uint64_t d_scratch = in_bytes, d_out = d_scratch + a256(scratch);
+  const uint64_t p_parts = 0, p_carry = a256(sizeof(kdb_flush_part) * m),
+                 p_total = p_carry + a256(sizeof(kdb_flush_state) * nruns), out_bytes = p_total + 256;
+  const uint64_t d_frames = d_out + out_bytes, dev_bytes = d_frames + a256(frame_cap);
+  const uint64_t h_out = in_bytes, h_frames = h_out + out_bytes, host_bytes = h_frames + a256(frame_cap);
+  if (!stg_.reserve(host_bytes, dev_bytes)) return KDB_LZ4_EHIP;
+  char* hb = static_cast<char*>(stg_.host);
+  char* db = static_cast<char*>(stg_.dev);
+  auto H64 = [&](uint64_t o) { return reinterpret_cast<uint64_t*>(hb + o); };
+  auto H32 = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(hb + o); };
+  {
+    uint64_t ko = 0, co = 0;
+    for (uint32_t s = 0; s < nseg; s++) {
+      const ByteArray& k = batch[seg_head[seg_order[s]]].key;
+      H64(o_key_off)[s] = ko;
+      H32(o_key_len)[s] = (uint32_t)k.size_const();
+      memcpy(hb + o_keys + ko, k.data_const(), k.size_const());
+      ko += k.size_const();
+    }
+    for (uint32_t q = 0; q < m; q++) {
+      const Intake& e = batch[perm[q]];
+      const uint64_t c = e.chunk.size_const();
+      H64(o_chunk_off)[q] = co;
+      H32(o_chunk_len)[q] = (uint32_t)c;
+      H64(o_offset)[q] = e.offset_chunk;
+      H64(o_size)[q] = e.size_value;
+      memcpy(hb + o_chunks + co, e.chunk.data_const(), c);
+      co += c;
+    }
+    memcpy(H32(o_seg_first), seg_first.data(), 4ull * (nseg + 1));
+    memcpy(H32(o_run_first), run_first.data(), 4ull * (nruns + 1));
+    memcpy(hb + o_carry, carry.data(), sizeof(kdb_flush_state) * nruns);
+  }
+  void* st = stg_.stream;
+  auto D8 = [&](uint64_t o) { return reinterpret_cast<uint8_t*>(db + o); };
+  auto D32 = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(db + o); };
+  auto D64 = [&](uint64_t o) { return reinterpret_cast<uint64_t*>(db + o); };
+  int rc = kdb_lz4_memcpy_h2d(db, hb, in_bytes, st);
+  if (!rc)
+    rc = kdb_flush_parts_batch(st, D8(o_keys), D64(o_key_off), D32(o_key_len), D8(o_chunks), D64(o_chunk_off),
+                               D32(o_chunk_len), D64(o_offset), D64(o_size), D32(o_seg_first), D32(o_run_first),
+                               reinterpret_cast<const kdb_flush_state*>(db + o_carry), m, nseg, nruns, max_chunk,
+                               D8(d_scratch), scratch, raw_bytes,
+                               reinterpret_cast<kdb_flush_part*>(db + d_out + p_parts),
+                               reinterpret_cast<kdb_flush_state*>(db + d_out + p_carry), D8(d_frames),
+                               D64(d_out + p_total));
+  if (!rc) rc = kdb_lz4_memcpy_d2h(hb + h_out, db + d_out, out_bytes, st);
+  if (!rc) rc = kdb_lz4_stream_sync(st);
+  if (rc) return rc;
+  const uint64_t total = *H64(h_out + p_total);
+  if (total > frame_cap) return KDB_LZ4_EHIP;
+  if (total) {
+    rc = kdb_lz4_memcpy_d2h(hb + h_frames, db + d_frames, total, st);
+    if (!rc) rc = kdb_lz4_stream_sync(st);
+    if (rc) return rc;
+  }
+  // ---- results, in ticket order
+  const kdb_flush_part* parts = reinterpret_cast<const kdb_flush_part*>(hb + h_out + p_parts);
+  const kdb_flush_state* cout = reinterpret_cast<const kdb_flush_state*>(hb + h_out + p_carry);
+  for (uint32_t q = 0; q < m; q++) {
+    const kdb_flush_part& P = parts[q];
+    Intake& e = batch[perm[q]];
+    Result& r = out[perm[q]];
+    r.occ = P.occ;
+    r.svc = P.svc;
+    r.crc = P.crc;
+    r.mode = (uint8_t)P.mode;
+    r.status = P.status == 0 ? 0 : -1;
+    if (r.status) continue;
+    if (P.mode == KDB_FLUSH_FRAME) {
+      if (P.frame_at + P.size > total) return KDB_LZ4_EHIP;
+      char* b = new char[P.size];
+      memcpy(b, hb + h_frames + P.frame_at, P.size);
+      r.chunk_final = NewShallowCopyByteArray(b, P.size);
+    } else if (P.mode == KDB_FLUSH_DISABLED) {             // database.cc:201-206
+      char* b = new char[P.size];
+      memset(b, 0, 8);
+      memcpy(b + 8, e.chunk.data(), P.size - 8);
+      r.chunk_final = NewShallowCopyByteArray(b, P.size);
+    }
+  }
+  // each thread's state after its last run of the batch
+  for (uint32_t r = 0; r < nruns; r++) state_[run_tid[r]] = cout[r];
+  return KDB_LZ4_OK;
+}
+
+void Pipeline::complete(std::vector<Order>& orders) {
+  // the newest ticket among the orders (every Put order here was deferred)
+  bool any = false;
+  uint64_t newest = 0;
+  {
+    std::lock_guard<std::mutex> l(res_mu_);
+    for (const Order& o : orders) {
+      if (o.type != OrderType::Put) continue;
+      const uint64_t t = full_ticket(o.crc32);
+      if (!any || t > newest) newest = t;
+      any = true;
+    }
+  }
+  if (!any) return;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (processed_ <= newest) {
+      drain_ = true;
+      cv_work_.notify_one();
+      cv_done_.wait(lk, [&] { return processed_ > newest; });
+    }
+  }
+  std::lock_guard<std::mutex> l(res_mu_);
+  size_t dropped = 0;
+  std::vector<char> drop;
+  for (size_t i = 0; i < orders.size(); i++) {
+    Order& o = orders[i];
+    if (o.type != OrderType::Put) continue;
+    const uint64_t at = full_ticket(o.crc32) - res_base_;
+    Result* rp = at < res_.size() ? &res_[at] : nullptr;
+    if (!rp || rp->status != 0) {   // (no result: not an order of this pipeline; never written)
+      if (drop.empty()) drop.assign(orders.size(), 0);
+      drop[i] = 1;
+      dropped++;
+      if (rp) rp->consumed = true;
+      continue;
+    }
+    Result& r = *rp;
+    r.consumed = true;
+    if (r.mode == KDB_FLUSH_FRAME || r.mode == KDB_FLUSH_DISABLED) o.chunk = r.chunk_final;
+    o.offset_chunk = r.occ;
+    o.size_value_compressed = r.svc;
+    o.crc32 = r.crc;
+    r.chunk_final = ByteArray();
+  }
+  if (dropped) {
+    size_t w = 0;
+    for (size_t i = 0; i < orders.size(); i++) {
+      if (drop[i]) continue;
+      if (w != i) orders[w] = orders[i];
+      w++;
+    }
+    orders.resize(w);
+    log::emerg("LZ4FlushOrders()", "%zu orders dropped: their PutPartValidSize failed", dropped);
+  }
+  while (!res_.empty()) {
+    const uint32_t t = (uint32_t)res_base_;
+    auto c = cancelled_.find(t);
+    if (!res_.front().consumed && c == cancelled_.end()) break;
+    if (c != cancelled_.end()) cancelled_.erase(c);
+    res_.pop_front();
+    res_base_++;
+  }
+}
+
+// ---- registry: one pipeline per write buffer
+std::mutex g_mu;
+std::unordered_map<const void*, std::shared_ptr<Pipeline>> g_pipes;
+std::unordered_set<const void*> g_closed;
+
+std::shared_ptr<Pipeline> pipeline_of(const void* wb, bool create) {
+  std::lock_guard<std::mutex> l(g_mu);
+  auto it = g_pipes.find(wb);
+  if (it != g_pipes.end()) return it->second;
+  if (!create || g_closed.count(wb)) return nullptr;
+  int dev = 0;
+  if (kdb_lz4_get_device(&dev) != KDB_LZ4_OK) dev = 0;
+  auto p = std::make_shared<Pipeline>(dev);
+  g_pipes.emplace(wb, p);
+  return p;
 }
 
 }  // namespace
 
-void LZ4FlushOrders(const DatabaseOptions& db_options, std::vector<Order>& orders) {
-  std::vector<uint32_t> idx;
-  uint64_t key_bytes = 0, raw_bytes = 0, entry_cap = 0;
-  uint32_t max_chunk = 0;
-  for (uint32_t i = 0; i < orders.size(); i++) {
-    Order& o = orders[i];
-    if (o.type != OrderType::Put || o.size_value_compressed != 0 ||
-        !LZ4FlushDeferrable(db_options, o.chunk.size(), o.offset_chunk, o.size_value))
-      continue;
-    idx.push_back(i);
-    key_bytes += o.key.size();
-    raw_bytes += o.chunk.size();
-    entry_cap += 64 + o.key.size() + o.chunk.size() + (o.chunk.size() / 65536 + 1) * 8;
-    if (o.chunk.size() > max_chunk) max_chunk = (uint32_t)o.chunk.size();
+Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArray& key, ByteArray& chunk,
+                     uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket) {
+  (void)db_options;
+  thread_local const void* t_wb = nullptr;
+  thread_local std::weak_ptr<Pipeline> t_pipe;
+  std::shared_ptr<Pipeline> p = t_wb == wb ? t_pipe.lock() : nullptr;
+  if (!p) {
+    p = pipeline_of(wb, true);
+    if (!p) return Status::IOError("Cannot handle request: WriteBuffer is closing");
+    t_wb = wb;
+    t_pipe = p;
   }
-  const uint32_t n = (uint32_t)idx.size();
-  if (n == 0) return;
+  return p->defer(key, chunk, offset_chunk, size_value, ticket);
+}
 
-  // host / device layout (device mirrors the inputs, then scratch, entries, outputs):
-  //   key_off u64[n] value_off u64[n] value_len u64[n] key_len u32[n]
-  //   part_first u32[n+1] chunk_len u32[n] | keys | values
-  //   outputs: entry_off u64[n] entry_len u32[n] total u64 hashed u64[n] crc u32[n]
-  //            kind u32[n] status i32[n]
-  const uint64_t o_key_off = 0, o_value_off = a256(8ull * n), o_value_len = o_value_off + a256(8ull * n),
-                 o_key_len = o_value_len + a256(8ull * n), o_part_first = o_key_len + a256(4ull * n),
-                 o_chunk_len = o_part_first + a256(4ull * n + 4), o_keys = o_chunk_len + a256(4ull * n),
-                 o_values = o_keys + a256(key_bytes), in_bytes = o_values + a256(raw_bytes);
-  const uint64_t p_entry_off = 0, p_entry_len = a256(8ull * n), p_total = p_entry_len + a256(4ull * n),
-                 p_hashed = p_total + 256, p_crc = p_hashed + a256(8ull * n), p_kind = p_crc + a256(4ull * n),
-                 p_status = p_kind + a256(4ull * n), out_meta = p_status + a256(4ull * n);
-  const uint64_t scratch_bytes = kdb_put_scratch_bytes(n, n, raw_bytes);
-  const uint64_t d_scratch = in_bytes, d_entries = d_scratch + a256(scratch_bytes),
-                 d_out = d_entries + a256(entry_cap), dev_bytes = d_out + out_meta;
-  // host: inputs, then the outputs' copy-back, then the entries' copy-back
-  const uint64_t h_out = in_bytes, h_entries = h_out + out_meta, host_bytes = h_entries + a256(entry_cap);
+void LZ4FlushCancel(const void* wb, uint32_t ticket) {
+  std::shared_ptr<Pipeline> p = pipeline_of(wb, false);
+  if (p) p->cancel(ticket);
+}
 
-  thread_local FlushStaging stg;
-  if (!stg.reserve(host_bytes, dev_bytes)) fatal("GPU staging allocation failed");
-  char* hb = static_cast<char*>(stg.host);
-  char* db = static_cast<char*>(stg.dev);
-  uint64_t* key_off = reinterpret_cast<uint64_t*>(hb + o_key_off);
-  uint64_t* value_off = reinterpret_cast<uint64_t*>(hb + o_value_off);
-  uint64_t* value_len = reinterpret_cast<uint64_t*>(hb + o_value_len);
-  uint32_t* key_len = reinterpret_cast<uint32_t*>(hb + o_key_len);
-  uint32_t* part_first = reinterpret_cast<uint32_t*>(hb + o_part_first);
-  uint32_t* chunk_len = reinterpret_cast<uint32_t*>(hb + o_chunk_len);
-  uint64_t ko = 0, vo = 0;
-  for (uint32_t j = 0; j < n; j++) {
-    Order& o = orders[idx[j]];
-    key_off[j] = ko;
-    key_len[j] = (uint32_t)o.key.size();
-    memcpy(hb + o_keys + ko, o.key.data(), o.key.size());
-    ko += o.key.size();
-    value_off[j] = vo;
-    value_len[j] = o.chunk.size();
-    chunk_len[j] = (uint32_t)o.chunk.size();
-    part_first[j] = j;
-    memcpy(hb + o_values + vo, o.chunk.data(), o.chunk.size());
-    vo += o.chunk.size();
+void LZ4FlushOrders(const void* wb, const DatabaseOptions& db_options, std::vector<Order>& orders) {
+  if (!LZ4FlushDeferrable(db_options) || orders.empty()) return;
+  std::shared_ptr<Pipeline> p = pipeline_of(wb, false);
+  if (p) p->complete(orders);
+}
+
+LZ4FlushScope::LZ4FlushScope(const void* wb, const DatabaseOptions& db_options) : wb_(wb) {
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    g_closed.erase(wb);
   }
-  part_first[n] = n;
+  if (LZ4FlushDeferrable(db_options)) pipeline_of(wb, true);
+}
 
-  void* st = stg.stream;
-  auto U8 = [&](uint64_t off) { return reinterpret_cast<uint8_t*>(db + off); };
-  auto U32 = [&](uint64_t off) { return reinterpret_cast<uint32_t*>(db + off); };
-  auto U64 = [&](uint64_t off) { return reinterpret_cast<uint64_t*>(db + off); };
-  int rc = kdb_lz4_memcpy_h2d(db, hb, in_bytes, st);
-  if (!rc)
-    rc = kdb_put_entries_batch(st, U8(o_keys), U64(o_key_off), U32(o_key_len), U8(o_values), U64(o_value_off),
-                               U64(o_value_len), U32(o_part_first), U32(o_chunk_len), n, max_chunk, n,
-                               db_options.hash == kxxHash_64 ? 1u : 0u, U8(d_scratch), scratch_bytes, raw_bytes,
-                               U8(d_entries), U64(d_out + p_entry_off), U32(d_out + p_entry_len),
-                               U64(d_out + p_total), U64(d_out + p_hashed), U32(d_out + p_crc),
-                               U32(d_out + p_kind), reinterpret_cast<int32_t*>(db + d_out + p_status));
-  if (!rc) rc = kdb_lz4_memcpy_d2h(hb + h_out, db + d_out, out_meta, st);
-  if (!rc) rc = kdb_lz4_stream_sync(st);
-  if (rc) fatal("kdb_put_entries_batch failed: " + std::to_string(rc));
-  const uint64_t* entry_off = reinterpret_cast<const uint64_t*>(hb + h_out + p_entry_off);
-  const uint32_t* entry_len = reinterpret_cast<const uint32_t*>(hb + h_out + p_entry_len);
-  const uint64_t total = *reinterpret_cast<const uint64_t*>(hb + h_out + p_total);
-  const uint32_t* crc = reinterpret_cast<const uint32_t*>(hb + h_out + p_crc);
-  const uint32_t* kind = reinterpret_cast<const uint32_t*>(hb + h_out + p_kind);
-  const int32_t* status = reinterpret_cast<const int32_t*>(hb + h_out + p_status);
-  if (total > entry_cap) fatal("entry stream larger than its bound");
-  rc = kdb_lz4_memcpy_d2h(hb + h_entries, db + d_entries, total, st);
-  if (!rc) rc = kdb_lz4_stream_sync(st);
-  if (rc) fatal("entry copy-back failed: " + std::to_string(rc));
-
-  for (uint32_t j = 0; j < n; j++) {
-    Order& o = orders[idx[j]];
-    const uint64_t klen = o.key.size(), S = o.chunk.size();
-    const uint64_t hl = self_contained_header_len(klen, S);
-    if (status[j] != 0 || kind[j] != KDB_PUT_SELF_CONTAINED || entry_len[j] < hl + klen + 8)
-      fatal("unexpected entry for a single-part value (status " + std::to_string(status[j]) + ")");
-    const uint64_t stored = entry_len[j] - hl - klen;   // |chunk_final|: frame, or 8 + S when disabled
-    if (stored > S + (S / 65536 + 1) * 8) fatal("chunk_final beyond the value's space");
-    char* chunk_final = new char[stored];
-    memcpy(chunk_final, hb + h_entries + entry_off[j] + hl + klen, stored);
-    o.chunk = NewShallowCopyByteArray(chunk_final, stored);
-    o.size_value_compressed = stored;
-    o.crc32 = crc[j];
+LZ4FlushScope::~LZ4FlushScope() {
+  std::shared_ptr<Pipeline> p;
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    auto it = g_pipes.find(wb_);
+    if (it != g_pipes.end()) {
+      p = it->second;
+      g_pipes.erase(it);
+    }
+    g_closed.insert(wb_);
   }
+  p.reset();   // the last reference stops and joins the worker (a client still in defer() holds its own)
 }
 
 }  // namespace kdb

@@ -1,48 +1,79 @@
 // kingdb_amd/kingdb_include/cache/lz4_flush.h -- the write-buffer flush hook
-// (SURVEY.md §8 row f3): LZ4 compression, the value CRC32C and
-// size_value_compressed of single-part puts move from the client thread
+// (SURVEY.md §8 row f3): the LZ4 frames, the disable rule, the offsets,
+// size_value_compressed and the CRC32C of every put -- single-part values and
+// the parts of multipart ones -- move from the client thread
 // (Database::PutPartValidSize, /root/reference/interface/database.cc:128-276)
-// to the write buffer's flush (WriteBuffer::ProcessingLoop,
-// /root/reference/cache/write_buffer.cc:228-319), where a whole buffer's worth
-// of values goes to the GPU as ONE kdb_put_entries_batch call.
+// to a per-database pipeline that batches them to the GPU while the write
+// buffer fills, and that the buffer's flush (WriteBuffer::ProcessingLoop,
+// /root/reference/cache/write_buffer.cc:228-319) completes the orders from.
 //
-// Two call sites in KingDB (oracle/kingdb_hook.py applies them to a copy of
-// the reference tree; INTEGRATION.md level 4):
-//   * PutPartValidSize: a deferrable chunk (LZ4FlushDeferrable) is handed to
-//     WriteBuffer::PutPart raw, with size_value_compressed 0 and crc32 0.  An
-//     order like that is self-contained (util/order.h:52-59) and, while it sits
-//     in the buffer, WriteBuffer::Get (write_buffer.cc:59-64, 105-110) returns
-//     it as an uncompressed value: read-your-writes sees the raw bytes.
-//   * ProcessingLoop: the orders handed to the storage engine are a copy of the
-//     flush buffer passed through LZ4FlushOrders, which turns every pending
-//     order into exactly the order PutPartValidSize would have queued (chunk =
-//     the frame or the disabled-compression form, size_value_compressed, crc32).
-//     The buffer itself is not modified, so concurrent readers keep seeing the
-//     raw bytes until the buffer is cleared.
+// Call sites in KingDB (oracle/kingdb_hook.py applies them to a copy of the
+// reference tree; INTEGRATION.md level 4):
+//   * PutPartValidSize, LZ4 on (LZ4FlushDeferrable): LZ4FlushDefer takes the
+//     part (key, chunk, offsets) and returns a ticket; the chunk goes to
+//     WriteBuffer::PutPart raw, with size_value_compressed 0 and the ticket in
+//     the crc32 field (WriteBuffer::Get never reads it).  While it sits in the
+//     buffer such an order reads like the reference's: a single-part value is
+//     self-contained with svc 0, so WriteBuffer::Get (write_buffer.cc:59-64,
+//     99-104) returns its raw bytes; a part of a multipart value is not
+//     self-contained, so Get reports NotFound, as for the reference's parts.
+//   * ProcessingLoop, before the buffer is handed to the storage engine: with
+//     the buffer's readers held off (the same level-4/level-5 protocol as its
+//     clear, :269-278), LZ4FlushOrders turns every deferred order into exactly
+//     the order PutPartValidSize would have queued (chunk = the frame, the
+//     all-zero-header form or the raw chunk; offset_chunk = the compressed
+//     offset; size_value_compressed; crc32).  LZ4FlushScope, a local of
+//     ProcessingLoop, owns the pipeline's lifetime.
+// The per-thread state PutPartValidSize keeps in ThreadStorage
+// (ts_compression_enabled_, ts_offset_, the compressor's running total, the
+// CRC) is carried by the pipeline per Order::tid, in call order, across
+// batches: a multipart value may straddle any number of flushes.
 #ifndef KINGDB_LZ4_FLUSH_H_
 #define KINGDB_LZ4_FLUSH_H_
 
+#include <cstdint>
 #include <vector>
 
+#include "util/byte_array.h"
 #include "util/options.h"
 #include "util/order.h"
+#include "util/status.h"
 
 namespace kdb {
 
-// Values above this stay on PutPartValidSize's own path (one GPU call each).
-constexpr uint64_t kLZ4FlushMaxValue = 64ull << 20;
-
-// A chunk that is a whole value (first and last part), LZ4 on, not empty.
-inline bool LZ4FlushDeferrable(const DatabaseOptions& db_options, uint64_t size_chunk, uint64_t offset_chunk,
-                               uint64_t size_value) {
-  return db_options.compression.type == kLZ4Compression && offset_chunk == 0 && size_chunk == size_value &&
-         size_chunk > 0 && size_chunk <= kLZ4FlushMaxValue;
+// Every part of every put goes through the pipeline when the database uses LZ4.
+inline bool LZ4FlushDeferrable(const DatabaseOptions& db_options) {
+  return db_options.compression.type == kLZ4Compression;
 }
 
-// Completes the deferred orders in `orders` in one GPU batch.  A GPU failure
-// is fatal (log::emerg + abort): an order must never reach an HSTable without
-// its frame and checksum.
-void LZ4FlushOrders(const DatabaseOptions& db_options, std::vector<Order>& orders);
+// Client thread.  Queues one PutPartValidSize call; *ticket goes into the
+// order's crc32 field.  IOError once the pipeline has failed for good (a GPU
+// batch that failed twice): the write is refused, as the reference refuses a
+// put whose compression fails (database.cc:189).
+Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArray& key, ByteArray& chunk,
+                     uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket);
+// The order of `ticket` never reached the buffer (WriteBuffer::PutPart failed).
+void LZ4FlushCancel(const void* wb, uint32_t ticket);
+
+// Flush thread, buffer readers held off.  Completes every deferred order of
+// `orders` in place; an order whose PutPartValidSize call fails (IOError
+// there, or a GPU batch that failed twice) is removed, so no order reaches an
+// HSTable without its frame and checksum.  Never aborts.
+void LZ4FlushOrders(const void* wb, const DatabaseOptions& db_options, std::vector<Order>& orders);
+
+// ProcessingLoop's local: creates the pipeline (GPU stream, staging, worker
+// thread) when the write buffer starts, and drains and stops it when the loop
+// returns (WriteBuffer::Close).
+class LZ4FlushScope {
+ public:
+  LZ4FlushScope(const void* wb, const DatabaseOptions& db_options);
+  ~LZ4FlushScope();
+  LZ4FlushScope(const LZ4FlushScope&) = delete;
+  LZ4FlushScope& operator=(const LZ4FlushScope&) = delete;
+
+ private:
+  const void* wb_;
+};
 
 }  // namespace kdb
 

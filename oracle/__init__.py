@@ -75,6 +75,11 @@ class Oracle:
         lib.orc_get_value.argtypes = [_u8p, c.c_uint64, c.c_uint64, c.c_uint64, c.c_uint32, c.c_uint32, c.c_int, _u8p,
                                       ctypes.POINTER(c.c_uint64)]
         lib.orc_get_value.restype = c.c_int
+        lib.orc_put_part.argtypes = [c.c_void_p, _u8p, c.c_uint32, _u8p, c.c_uint64, c.c_uint64, c.c_uint64, _u8p,
+                                     ctypes.POINTER(c.c_uint32), ctypes.POINTER(c.c_uint64),
+                                     ctypes.POINTER(c.c_uint64), ctypes.POINTER(c.c_uint64),
+                                     ctypes.POINTER(c.c_uint32)]
+        lib.orc_put_part.restype = c.c_int
         self.lib = lib
 
     def compress_bound(self, n: int) -> int:
@@ -179,6 +184,24 @@ class Oracle:
         parts = [(int(po[i]), stored[int(po[i]):int(po[i]) + int(pl[i])].tobytes()) for i in range(n)]
         return {"parts": parts, "svc": svc.value, "crc": crc.value,
                 "stored": stored[: len(value) + self.padding(len(value))].tobytes()}
+
+
+class PutState(ctypes.Structure):
+    """orc_put_state: one client thread's PutPartValidSize state (all 0 = ThreadStorage defaults)."""
+    _fields_ = [("ts_offset", ctypes.c_uint64), ("comp_total", ctypes.c_uint64), ("enabled", ctypes.c_uint32),
+                ("crc", ctypes.c_uint32)]
+
+
+def put_part(orc: "Oracle", state: PutState, key: bytes, chunk: bytes, offset_chunk: int, size_value: int) -> dict:
+    """One Database::PutPartValidSize call (orc_put_part): {"rc", "mode", "occ", "chunk_final", "svc", "crc"}."""
+    fin = np.zeros(8 + orc.compress_bound(len(chunk)) + 64, np.uint8)
+    mode, crc = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    occ, fsz, svc = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    rc = orc.lib.orc_put_part(ctypes.byref(state), _ptr(orc._buf(key)), len(key), _ptr(orc._buf(chunk)), len(chunk),
+                              offset_chunk, size_value, _ptr(fin), ctypes.byref(mode), ctypes.byref(occ),
+                              ctypes.byref(fsz), ctypes.byref(svc), ctypes.byref(crc))
+    return {"rc": rc, "mode": mode.value, "occ": occ.value, "chunk_final": fin[: fsz.value].tobytes(),
+            "svc": svc.value, "crc": crc.value}
 
 
 def _digest(fn, src: np.ndarray, off: np.ndarray, lens: np.ndarray) -> tuple[int, int]:

@@ -180,6 +180,20 @@ class Writer:
             lastcall = i == n - 1
             self._order(key, final, occ, len(value), pv["svc"] if lastcall else 0, pv["crc"] if lastcall else 0)
 
+    def put_calls(self, state, key: bytes, value: bytes, chunks: list[int] | None = None) -> None:
+        """The same, one Database::PutPartValidSize call per chunk over a client
+        thread's carried state (oracle.put_part / orc_put_part): the per-call
+        restatement the flush hook's batch (include/kdb_flush.h) is checked against."""
+        import oracle
+        chunks = [len(value)] if chunks is None else list(chunks)
+        off = 0
+        for c in chunks:
+            r = oracle.put_part(self.orc, state, key, value[off:off + c], off, len(value))
+            off += c
+            if r["rc"] != 0:
+                raise RuntimeError("PutPartValidSize IOError")
+            self._order(key, r["chunk_final"], r["occ"], len(value), r["svc"], r["crc"])
+
     def dense(self):
         """The per-value view the GPU put path produces (kdb_put_entries_batch):
         (entry bytes, key hash, kind) per first-part order, in order; call after close()."""

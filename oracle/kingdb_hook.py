@@ -11,12 +11,14 @@ the repo; oracle/Makefile `kingdb_hook` compiles the copies into
 oracle/_ref/kingdb_hook/ beside the untouched rest of the tree.
 
 The edits, each anchored on text that must occur exactly once:
-  database.cc, Database::PutPartValidSize (:128-276): before the compression
-    block, a deferrable chunk (LZ4FlushDeferrable) goes to WriteBuffer::PutPart
-    raw, with size_value_compressed 0 and crc32 0;
-  write_buffer.cc, WriteBuffer::ProcessingLoop (:228-319): the storage engine
-    receives a copy of the flush buffer passed through LZ4FlushOrders (one
-    kdb_put_entries_batch for the deferred orders) instead of the buffer.
+  database.cc, Database::PutPartValidSize (:128-276): with LZ4 on, before the
+    compression block, the call is queued to the pipeline (LZ4FlushDefer) and
+    the chunk goes to WriteBuffer::PutPart raw, with size_value_compressed 0
+    and the pipeline's ticket in the crc32 field;
+  write_buffer.cc, WriteBuffer::ProcessingLoop (:228-319): the pipeline lives
+    as long as the loop (LZ4FlushScope), and before the buffer is handed to the
+    storage engine, with its readers held off, LZ4FlushOrders completes the
+    deferred orders in place.
 INTEGRATION.md level 4 shows the same edits as a diff for a maintainer.
 """
 import os
@@ -30,18 +32,36 @@ EDITS = {
     "interface/database.cc": [
         ('#include "interface/database.h"\n', '#include "interface/database.h"\n' + INCLUDE),
         ("  bool do_compression = true;\n  uint64_t size_value_compressed = 0;\n",
-         "  if (LZ4FlushDeferrable(db_options_, chunk.size(), offset_chunk, size_value)) {\n"
-         "    // frame, CRC32C and size_value_compressed at the flush (LZ4FlushOrders)\n"
-         "    return wb_->PutPart(write_options, key, chunk, 0, size_value, 0, 0);\n"
+         "  if (LZ4FlushDeferrable(db_options_)) {\n"
+         "    // frame, offsets, size_value_compressed and CRC32C at the flush (LZ4FlushOrders);\n"
+         "    // the order carries its ticket in the crc32 field until then\n"
+         "    uint32_t lz4_ticket = 0;\n"
+         "    s = LZ4FlushDefer(wb_, db_options_, key, chunk, offset_chunk, size_value, &lz4_ticket);\n"
+         "    if (!s.IsOK()) return s;\n"
+         "    s = wb_->PutPart(write_options, key, chunk, offset_chunk, size_value, 0, lz4_ticket);\n"
+         "    if (!s.IsOK()) LZ4FlushCancel(wb_, lz4_ticket);\n"
+         "    return s;\n"
          "  }\n"
          "  bool do_compression = true;\n  uint64_t size_value_compressed = 0;\n"),
     ],
     "cache/write_buffer.cc": [
         ('#include "cache/write_buffer.h"\n', '#include "cache/write_buffer.h"\n' + INCLUDE),
+        ("void WriteBuffer::ProcessingLoop() {\n",
+         "void WriteBuffer::ProcessingLoop() {\n"
+         "  LZ4FlushScope lz4_flush_scope(this, db_options_);   // the LZ4 pipeline lives as long as this loop\n"),
         ("    event_manager_->flush_buffer.StartAndBlockUntilDone(buffers_[im_copy_]);\n",
-         "    std::vector<Order> flushed(buffers_[im_copy_]);\n"
-         "    LZ4FlushOrders(db_options_, flushed);\n"
-         "    event_manager_->flush_buffer.StartAndBlockUntilDone(flushed);\n"),
+         "    {\n"
+         "      // the deferred puts become the orders PutPartValidSize would have queued;\n"
+         "      // the buffer's readers wait outside, as for its clear below\n"
+         "      std::unique_lock<std::mutex> lock_copy(mutex_copy_write_level4_);\n"
+         "      while (true) {\n"
+         "        std::unique_lock<std::mutex> lock_read(mutex_copy_read_level5_);\n"
+         "        if (num_readers_ == 0) break;\n"
+         "        cv_read_.wait(lock_read);\n"
+         "      }\n"
+         "      LZ4FlushOrders(this, db_options_, buffers_[im_copy_]);\n"
+         "    }\n"
+         "    event_manager_->flush_buffer.StartAndBlockUntilDone(buffers_[im_copy_]);\n"),
     ],
 }
 

@@ -555,6 +555,63 @@ int orc_put_value(const uint8_t* key, uint32_t klen, const uint8_t* value, uint6
 }
 
 /*
+ * One Database::PutPartValidSize call (interface/database.cc:128-276) over a
+ * client thread's state -- the four ThreadStorage slots it reads and writes
+ * (ts_compression_enabled_, ts_offset_, the compressor's ts_compress_ and
+ * crc32_'s value; thread/threadstorage.h:23-46, all 0 for a thread that never
+ * called).  Unlike orc_put_value (one well-formed value) this takes parts in
+ * any order a client may send them, which is what the flush hook's batch
+ * (include/kdb_flush.h) must match call for call.  LZ4 on.
+ * Outputs: chunk_final into `fin` (capacity 8 + bound(csz)), *mode (0 frame,
+ * 1 all-zero header + raw, 2 raw, 3 Compress failed), *occ, *fsz, *svc, *crc
+ * (the crc32 argument: the running CRC at a last part, else 0).  Returns 0, or
+ * -1 where the call returns IOError (mode 3: at :189, before the CRC; else at
+ * :261-267, after it).
+ */
+typedef struct orc_put_state { uint64_t ts_offset, comp_total; uint32_t enabled, crc; } orc_put_state;
+int orc_put_part(orc_put_state* st, const uint8_t* key, uint32_t klen, const uint8_t* chunk, uint64_t csz,
+                 uint64_t offset_chunk, uint64_t size_value, uint8_t* fin, uint32_t* mode, uint64_t* occ_out,
+                 uint64_t* fsz_out, uint64_t* svc_out, uint32_t* crc_out) {
+  const uint64_t pad = orc_padding(size_value);
+  const int first = offset_chunk == 0, last = csz + offset_chunk == size_value;
+  const int do_comp = csz != 0;                                       /* :154-157 */
+  uint64_t occ = offset_chunk, fsz = csz, svc = 0;
+  *mode = 2;
+  if (first) { st->enabled = 1; st->ts_offset = 0; }                  /* :159-162 */
+  if (!st->enabled) { occ = st->ts_offset; st->ts_offset = occ + csz; }   /* :164-171 */
+  if (do_comp && st->enabled) {
+    if (first) st->comp_total = 0;                                    /* :177-179 */
+    occ = st->comp_total;                                             /* :182 */
+    const int64_t F = orc_frame_compress(chunk, csz, fin);            /* :185-189 */
+    if (F < 0) { *mode = 3; *occ_out = occ; *fsz_out = 0; *svc_out = 0; *crc_out = 0; return -1; }
+    st->comp_total += (uint64_t)F;
+    const uint64_t size_remaining = size_value - offset_chunk;        /* :197-199 */
+    const uint64_t space_left = size_value + pad - occ;
+    if (size_remaining - csz + 8u > space_left - (uint64_t)F) {       /* :199-209 */
+      st->comp_total -= (uint64_t)F;
+      fsz = csz + 8u;
+      st->enabled = 0;
+      st->ts_offset = st->comp_total + fsz;
+      memset(fin, 0, 8);
+      memcpy(fin + 8, chunk, csz);
+      *mode = 1;
+    } else {
+      fsz = (uint64_t)F;
+      *mode = 0;
+    }
+  }
+  if (*mode == 2 && csz) memcpy(fin, chunk, csz);
+  if (do_comp && last) svc = st->enabled ? st->comp_total : (first ? st->ts_offset : occ + csz);   /* :237-248 */
+  if (first) st->crc = orc_crc32c_extend(0, key, klen);               /* :251-255 */
+  st->crc = orc_crc32c_extend(st->crc, fin, fsz);                     /* :256 */
+  *crc_out = last ? st->crc : 0u;                                     /* :257 */
+  *occ_out = occ;
+  *fsz_out = fsz;
+  *svc_out = svc;
+  return occ + fsz > size_value + (do_comp ? pad : 0) ? -1 : 0;       /* :261-267 */
+}
+
+/*
  * CompressorLZ4::UncompressByteArray (algorithm/compressor.cc:140-249) over
  * CompressorLZ4::Uncompress (compressor.cc:75-137): the read of one stored
  * value (Database::GetRaw, interface/database.cc:65-68).  `stored` holds

@@ -52,6 +52,53 @@ def oracle_writer(orc, puts, hs, ht, batch=None):
 
 
 @pytest.mark.parametrize("name", sorted(GOLDEN))
+def test_oracle_per_call_matches_reference_hstables(orc, name):
+    """orc_put_part (one PutPartValidSize call over carried thread state, the
+    checker of the flush hook's batch) writes the reference's files too."""
+    import oracle
+    from oracle import hstable
+    puts, hs, ht, files = GOLDEN[name]
+    w = hstable.Writer(orc, hs, ht)
+    st = oracle.PutState()
+    for k, v, ch in puts:
+        w.put_calls(st, k, v, ch)
+    w._flush(0, 0)
+    got = w.close()
+    assert got == files
+
+
+def test_oracle_per_call_matches_put_value(orc):
+    """Random values and chunkings (incompressible tails disable compression mid-value):
+    orc_put_part call by call equals orc_put_value for the whole value."""
+    import oracle
+    rng = np.random.default_rng(11)
+    pool = orc.g1_pieces(30000).tobytes()
+    st = oracle.PutState()
+    for t in range(300):
+        n = int(rng.integers(0, 200000))
+        a = int(rng.integers(0, len(pool) - n)) if n < len(pool) else 0
+        v = bytearray(pool[a:a + n])
+        if n and t % 3 == 0:                      # an incompressible stretch
+            b = int(rng.integers(0, n))
+            v[b:] = rng.integers(0, 256, n - b, dtype=np.uint8).tobytes()
+        v = bytes(v)
+        cuts = sorted(set(int(x) for x in rng.integers(0, n + 1, int(rng.integers(0, 6))))) if n else []
+        ch = [b - a for a, b in zip([0] + cuts, cuts + [n])] if n else [0]
+        want = orc.put_value(b"k%d" % t, v, ch)
+        off = 0
+        for i, c in enumerate(ch):
+            r = oracle.put_part(orc, st, b"k%d" % t, v[off:off + c], off, n)
+            assert r["rc"] == 0
+            assert (r["occ"], r["chunk_final"]) == want["parts"][i]
+            last = i == len(ch) - 1
+            assert r["svc"] == (want["svc"] if last and c else 0) or not last
+            off += c
+        if ch and ch[-1]:
+            assert r["svc"] == want["svc"]
+        assert r["crc"] == want["crc"]
+
+
+@pytest.mark.parametrize("name", sorted(GOLDEN))
 def test_oracle_matches_reference_hstables(orc, name):
     puts, hs, ht, files = GOLDEN[name]
     _, got = oracle_writer(orc, puts, hs, ht)
