@@ -22,6 +22,7 @@ from . import _lib
 from .lz4 import DeviceBuffer
 
 FRAME, DISABLED, RAW, FAILED = 0, 1, 2, 3
+_last: dict = {}   # the last batch's raw outputs (diagnostics)
 
 
 class FlushState(ctypes.Structure):
@@ -143,6 +144,7 @@ def flush_parts(calls, states=None):
     couts = (FlushState * nruns).from_buffer_copy(
         out[o_carry:o_carry + ctypes.sizeof(FlushState) * nruns].tobytes())
     total = int(out[o_total:o_total + 8].view(np.uint64)[0])
+    _last.update(parts=parts, frames=frames, total=total, perm=perm, chunks=chunks)
     res = [None] * m
     for q, i in enumerate(perm):
         P = parts[q]
