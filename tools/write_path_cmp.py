@@ -17,7 +17,9 @@ parent (--dir; default: the current directory, i.e. the box's local disk;
 /dev/shm for tmpfs), and the three databases' files must be identical.
 Prints one JSON object per (workload, build) and a summary line.
 
-  python tools/write_path_cmp.py [--n 1048576] [--sizes 100,4096] [--dir DIR]
+  python tools/write_path_cmp.py [--n 1048576] [--sizes 100,4096,mp3072x262144/65536] [--dir DIR]
+
+(mp<N>x<V>/<P>: N values of V bytes, each sent as PutPart calls of P bytes.)
 """
 import argparse
 import json
@@ -55,32 +57,80 @@ def stream(n: int, ks: int, vs: int) -> np.ndarray:
     return rec
 
 
+def mp_stream(n: int, ks: int, vs: int, part: int) -> np.ndarray:
+    """n values of vs bytes, each sent as PutPart calls of `part` bytes
+    (KingServer's 64 KiB receive parts, network/server.cc:258; MultipartWriter,
+    interface/multipart.h:200-224), keys %016d-style, G1 values."""
+    import oracle
+    orc = oracle.Oracle()
+    pool = np.frombuffer(oracle.g1_pool(orc, 8 << 20), np.uint8)
+    rng = np.random.default_rng(9)
+    starts = rng.integers(0, len(pool) - vs, n)
+    nch = (vs + part - 1) // part
+    rec_len = 4 + ks + 8 + 4 + nch * 4 + vs
+    rec = np.zeros((n, rec_len), np.uint8)
+    rec[:, 0:4] = np.frombuffer(struct.pack("<I", ks), np.uint8)
+    rec[:, 4:4 + ks] = np.frombuffer(b"".join(b"%016d" % i for i in range(n)), np.uint8).reshape(n, 16)[:, :ks]
+    rec[:, 4 + ks:12 + ks] = np.frombuffer(struct.pack("<Q", vs), np.uint8)
+    rec[:, 12 + ks:16 + ks] = np.frombuffer(struct.pack("<I", nch), np.uint8)
+    at = 16 + ks
+    for c in range(nch):
+        cl = min(part, vs - c * part)
+        rec[:, at:at + 4] = np.frombuffer(struct.pack("<I", cl), np.uint8)
+        for i in range(n):
+            rec[i, at + 4:at + 4 + cl] = pool[starts[i] + c * part:starts[i] + c * part + cl]
+        at += 4 + cl
+    return rec
+
+
+# Bytes [72, 8192) of an HSTable's header block are whatever the reference's
+# write buffer held there (hstable_manager.h:77, 280-289: never written), so
+# they are not compared (tests/test_kingdb_dropin.py, HEADER_DEFINED).
 def files_of(db: str) -> dict:
-    return {f: open(os.path.join(db, f), "rb").read() for f in sorted(os.listdir(db))
-            if len(f) == 8 and all(c in "0123456789abcdef" for c in f)}
+    out = {}
+    for f in sorted(os.listdir(db)):
+        if len(f) == 8 and all(c in "0123456789abcdef" for c in f):
+            b = open(os.path.join(db, f), "rb").read()
+            out[f] = b[:72] + b[8192:] if len(b) >= 8192 else b
+    return out
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
-    ap.add_argument("--sizes", default="100,4096")
+    ap.add_argument("--sizes", default="100,4096,mp3072x262144/65536")
     ap.add_argument("--dir", default=".")
     ap.add_argument("--builds", default=",".join(BUILDS))
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     rows = []
-    for vs in (int(x) for x in a.sizes.split(",")):
-        n = a.n if vs <= 1024 else max(1, a.n // 8)
+    for size in a.sizes.split(","):
         d = tempfile.mkdtemp(prefix="kdbwp", dir=a.dir)
         try:
             sp = os.path.join(d, "s.bin")
-            stream(n, 16, vs).tofile(sp)
+            args = []
+            if size.startswith("mp"):            # mp<count>x<value bytes>/<part bytes>: multipart values
+                cnt, rest = size[2:].split("x")
+                vs, part = (int(x) for x in rest.split("/"))
+                n = int(cnt)
+                mp_stream(n, 16, vs, part).tofile(sp)
+                what = f"{n} values of {vs} B in {part} B PutPart parts, 16 B keys, G1"
+                # 256 MiB HSTables, and under the 1 GB of uncompacted data that starts a
+                # compaction (util/options.h:192): with the default 32 MiB HSTables the
+                # reference itself stops making progress on this stream once a third
+                # file opens (measured: 256 x 256 KiB values hang, 240 do not)
+                args = [str(1 << 20), str(256 << 20)]
+            else:
+                vs = int(size)
+                n = a.n if vs <= 1024 else max(1, a.n // 8)
+                stream(n, 16, vs).tofile(sp)
+                what = f"{n} puts 16 B keys / {vs} B G1 values"
             ref_files = None
             for b in a.builds.split(","):
                 exe = os.path.join(ROOT, "oracle", "_ref", b, "kdb_db")
                 db = os.path.join(d, "db_" + b)
                 t0 = time.perf_counter()
-                r = subprocess.run([exe, db, sp], capture_output=True, text=True, timeout=900)
+                r = subprocess.run([exe, db, sp] + args, capture_output=True, text=True, timeout=900)
                 wall = time.perf_counter() - t0
                 if r.returncode != 0:
                     print(r.stderr[-2000:], file=sys.stderr)
@@ -91,7 +141,7 @@ def main() -> None:
                 if ref_files is None:
                     ref_files = files
                 same = files == ref_files
-                row = {"workload": f"{n} puts 16 B keys / {vs} B G1 values", "build": b,
+                row = {"workload": what, "build": b,
                        "puts_per_s": round(n / t_put, 1), "puts_per_s_with_close": round(n / t_all, 1),
                        "seconds_put": round(t_put, 4), "seconds_with_close": round(t_all, 4),
                        "process_wall_s": round(wall, 3), "hstable_files": len(files),
