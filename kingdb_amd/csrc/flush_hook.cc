@@ -26,6 +26,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -50,7 +51,9 @@ constexpr auto kBatchAge = std::chrono::microseconds(1000);   // oldest waiting 
 
 inline uint64_t a256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
-// Pinned host + device staging of one pipeline, kept across batches.
+// Pinned host + device staging of one pipeline, kept across batches, and
+// handed to the next pipeline when a database closes (StagingPool): pinned
+// allocations cost milliseconds, a Close should not pay to free them.
 struct Staging {
   void* host = nullptr;
   void* dev = nullptr;
@@ -101,6 +104,45 @@ struct Staging {
   }
 };
 
+class StagingPool {
+ public:
+  static StagingPool& get() {
+    static StagingPool* p = new StagingPool();   // never destroyed: HIP may be gone at exit
+    return *p;
+  }
+  void put(int device, Staging& s) {
+    if (!s.stream) return;
+    std::lock_guard<std::mutex> l(mu_);
+    if (free_.size() >= 4) return;                 // (then s frees its own)
+    free_.push_back(Entry{device, s.host, s.dev, s.stream, s.hcap, s.dcap});
+    s.host = s.dev = s.stream = nullptr;
+    s.hcap = s.dcap = 0;
+  }
+  void take(int device, Staging& s) {
+    std::lock_guard<std::mutex> l(mu_);
+    for (size_t i = 0; i < free_.size(); i++)
+      if (free_[i].device == device) {
+        const Entry e = free_[i];
+        free_.erase(free_.begin() + (long)i);
+        s.host = e.host;
+        s.dev = e.dev;
+        s.stream = e.stream;
+        s.hcap = e.hcap;
+        s.dcap = e.dcap;
+        return;
+      }
+  }
+
+ private:
+  struct Entry {
+    int device;
+    void *host, *dev, *stream;
+    uint64_t hcap, dcap;
+  };
+  std::mutex mu_;
+  std::vector<Entry> free_;
+};
+
 struct Intake {
   std::thread::id tid;
   ByteArray key, chunk;
@@ -131,16 +173,42 @@ struct Inject {
   bool fails(uint64_t attempt) const { return first && attempt >= first && attempt - first < count; }
 };
 
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t).count();
+}
+
+// KDB_LZ4_FLUSH_STATS=1: where a pipeline's time went, printed to stderr when
+// it stops (tools/write_path_cmp.py --stats).
+struct Stats {
+  bool on = false;
+  uint64_t batches = 0, parts = 0, raw_bytes = 0, flushes = 0, orders = 0, waits = 0;
+  double gpu_ms = 0, stage_ms = 0, results_ms = 0, wait_ms = 0, complete_ms = 0;
+  Stats() {
+    const char* e = getenv("KDB_LZ4_FLUSH_STATS");
+    on = e && *e && *e != '0';
+  }
+};
+
 class Pipeline {
  public:
   explicit Pipeline(int device) : device_(device) { worker_ = std::thread(&Pipeline::run, this); }
   ~Pipeline() {
+    const Clock::time_point t0 = Clock::now();
     {
       std::lock_guard<std::mutex> l(mu_);
       stop_ = true;
     }
     cv_work_.notify_all();
     worker_.join();
+    if (stats_.on)
+      fprintf(stderr,
+              "lz4_flush_stats batches %llu parts %llu raw_bytes %llu stage_ms %.2f gpu_ms %.2f results_ms %.2f "
+              "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f\n",
+              (unsigned long long)stats_.batches, (unsigned long long)stats_.parts,
+              (unsigned long long)stats_.raw_bytes, stats_.stage_ms, stats_.gpu_ms, stats_.results_ms,
+              (unsigned long long)stats_.flushes, (unsigned long long)stats_.orders, (unsigned long long)stats_.waits,
+              stats_.wait_ms, stats_.complete_ms, ms_since(t0));
   }
 
   Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket) {
@@ -195,10 +263,12 @@ class Pipeline {
   Staging stg_;
   Inject inject_;
   uint64_t attempts_ = 0;
+  Stats stats_;
 };
 
 void Pipeline::run() {
   kdb_lz4_set_device(device_);
+  StagingPool::get().take(device_, stg_);
   std::vector<Intake> batch;
   for (;;) {
     uint64_t t0;
@@ -210,7 +280,10 @@ void Pipeline::run() {
             drain_ = false;
             cv_done_.notify_all();
           }
-          if (stop_) return;
+          if (stop_) {
+            StagingPool::get().put(device_, stg_);
+            return;
+          }
           cv_work_.wait(lk);
           continue;
         }
@@ -264,6 +337,7 @@ void Pipeline::process(std::vector<Intake>& batch, uint64_t t0) {
 // The batch through the GPU: layout (segments, runs), staging, one
 // kdb_flush_parts_batch, results.  0 or a KDB_LZ4_E* code.
 int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
+  const Clock::time_point t_start = Clock::now();
   ++attempts_;
   if (inject_.fails(attempts_)) return KDB_LZ4_EHIP;
   const uint32_t m = (uint32_t)batch.size();
@@ -381,6 +455,8 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     memcpy(H32(o_run_first), run_first.data(), 4ull * (nruns + 1));
     memcpy(hb + o_carry, carry.data(), sizeof(kdb_flush_state) * nruns);
   }
+  const double t_stage = ms_since(t_start);
+  const Clock::time_point t_gpu = Clock::now();
   void* st = stg_.stream;
   auto D8 = [&](uint64_t o) { return reinterpret_cast<uint8_t*>(db + o); };
   auto D32 = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(db + o); };
@@ -404,6 +480,8 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     if (!rc) rc = kdb_lz4_stream_sync(st);
     if (rc) return rc;
   }
+  const double t_gpu_ms = ms_since(t_gpu);
+  const Clock::time_point t_res = Clock::now();
   // ---- results, in ticket order
   const kdb_flush_part* parts = reinterpret_cast<const kdb_flush_part*>(hb + h_out + p_parts);
   const kdb_flush_state* cout = reinterpret_cast<const kdb_flush_state*>(hb + h_out + p_carry);
@@ -431,10 +509,17 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   }
   // each thread's state after its last run of the batch
   for (uint32_t r = 0; r < nruns; r++) state_[run_tid[r]] = cout[r];
+  stats_.batches++;
+  stats_.parts += m;
+  stats_.raw_bytes += raw_bytes;
+  stats_.stage_ms += t_stage;
+  stats_.gpu_ms += t_gpu_ms;
+  stats_.results_ms += ms_since(t_res);
   return KDB_LZ4_OK;
 }
 
 void Pipeline::complete(std::vector<Order>& orders) {
+  const Clock::time_point t0 = Clock::now();
   // the newest ticket among the orders (every Put order here was deferred)
   bool any = false;
   uint64_t newest = 0;
@@ -451,9 +536,12 @@ void Pipeline::complete(std::vector<Order>& orders) {
   {
     std::unique_lock<std::mutex> lk(mu_);
     if (processed_ <= newest) {
+      const Clock::time_point tw = Clock::now();
       drain_ = true;
       cv_work_.notify_one();
       cv_done_.wait(lk, [&] { return processed_ > newest; });
+      stats_.waits++;
+      stats_.wait_ms += ms_since(tw);
     }
   }
   std::lock_guard<std::mutex> l(res_mu_);
@@ -489,6 +577,9 @@ void Pipeline::complete(std::vector<Order>& orders) {
     orders.resize(w);
     log::emerg("LZ4FlushOrders()", "%zu orders dropped: their PutPartValidSize failed", dropped);
   }
+  stats_.flushes++;
+  stats_.orders += orders.size();
+  stats_.complete_ms += ms_since(t0);
   while (!res_.empty()) {
     const uint32_t t = (uint32_t)res_base_;
     auto c = cancelled_.find(t);

@@ -9,7 +9,8 @@
 // it to pin the write-path restatement (oracle/lz4_oracle.c orc_put_*) and the
 // GPU put kernels against the bytes the reference itself writes.
 //
-//   ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash]]]   (hash: 0 murmur3, 1 xxhash)
+//   ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash [none]]]]   (hash: 0 murmur3, 1 xxhash;
+//   none: compression off -- a diagnostic of what the write path costs without the codec)
 //
 // stream.bin: records of
 //   u32 key_len, key bytes, u64 size_value, u32 nchunks,
@@ -96,7 +97,7 @@ static int verify(int argc, char** argv) {
 int main(int argc, char** argv) {
   if (argc >= 4 && !strcmp(argv[1], "--verify")) return verify(argc, argv);
   if (argc < 3) {
-    fprintf(stderr, "usage: ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash]]]\n");
+    fprintf(stderr, "usage: ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash [none]]]]\n");
     return 2;
   }
   kdb::Logger::set_current_level("emerg");
@@ -105,6 +106,7 @@ int main(int argc, char** argv) {
   if (argc > 3) options.storage__maximum_part_size = strtoull(argv[3], nullptr, 0);
   if (argc > 4) options.storage__hstable_size = strtoull(argv[4], nullptr, 0);
   if (argc > 5) options.hash = strtoul(argv[5], nullptr, 0) ? kdb::kxxHash_64 : kdb::kMurmurHash3_64;
+  if (argc > 6 && !strcmp(argv[6], "none")) options.compression = kdb::kNoCompression;   // (diagnostics)
   kdb::Database db(options, argv[1]);
   kdb::Status s = db.Open();
   if (!s.IsOK()) {

@@ -90,7 +90,7 @@ for s in "$@"; do
       grep -E "PASSED|FAILED|passed|failed" "${O}_hook.log" | tail -30 ;;
     wpath)
       for d in /tmp /dev/shm; do
-        timeout -k 10 900 python -u tools/write_path_cmp.py --dir $d --out "${O}_wpath_${d//\//_}.json" > "${O}_wpath.log" 2>&1 || fail wpath $? "${O}_wpath.log"
+        timeout -k 10 900 python -u tools/write_path_cmp.py --ceiling --dir $d --out "${O}_wpath_${d//\//_}.json" > "${O}_wpath.log" 2>&1 || fail wpath $? "${O}_wpath.log"
         cat "${O}_wpath.log"
       done ;;
     rehearse2)

@@ -102,6 +102,7 @@ def main() -> None:
     ap.add_argument("--dir", default=".")
     ap.add_argument("--builds", default=",".join(BUILDS))
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ceiling", action="store_true", help="also run the reference with compression off")
     a = ap.parse_args()
     rows = []
     for size in a.sizes.split(","):
@@ -130,7 +131,8 @@ def main() -> None:
                 exe = os.path.join(ROOT, "oracle", "_ref", b, "kdb_db")
                 db = os.path.join(d, "db_" + b)
                 t0 = time.perf_counter()
-                r = subprocess.run([exe, db, sp] + args, capture_output=True, text=True, timeout=900)
+                env = dict(os.environ, KDB_LZ4_FLUSH_STATS="1") if b == "kingdb_hook" else None
+                r = subprocess.run([exe, db, sp] + args, capture_output=True, text=True, timeout=900, env=env)
                 wall = time.perf_counter() - t0
                 if r.returncode != 0:
                     print(r.stderr[-2000:], file=sys.stderr)
@@ -147,11 +149,33 @@ def main() -> None:
                        "process_wall_s": round(wall, 3), "hstable_files": len(files),
                        "hstable_bytes": sum(map(len, files.values())), "files_identical_to_first_build": same,
                        "dir": os.path.abspath(a.dir)}
+                for ln in r.stderr.splitlines():
+                    if ln.startswith("lz4_flush_stats "):
+                        w = ln.split()[1:]
+                        row["flush_stats"] = {k: float(v) for k, v in zip(w[::2], w[1::2])}
                 print(json.dumps(row), flush=True)
                 rows.append(row)
                 shutil.rmtree(db, ignore_errors=True)
                 if not same:
                     sys.exit(f"{b}: HSTable files differ from {a.builds.split(',')[0]}")
+            if a.ceiling:
+                # the same write path with compression off (reference build): what
+                # KingDB's write buffer and storage engine cost without any codec --
+                # the most any codec change can reach on this workload
+                exe = os.path.join(ROOT, "oracle", "_ref", "kingdb_ref", "kdb_db")
+                db = os.path.join(d, "db_none")
+                ca = args + [str(1 << 20), str(32 << 20)][len(args):] + ["1", "none"]
+                r = subprocess.run([exe, db, sp] + ca, capture_output=True, text=True, timeout=900)
+                if r.returncode == 0:
+                    f = r.stdout.split()
+                    t_put, t_all = float(f[2]), float(f[5])
+                    row = {"workload": what, "build": "kingdb_ref, compression off (ceiling)",
+                           "puts_per_s": round(n / t_put, 1), "puts_per_s_with_close": round(n / t_all, 1),
+                           "seconds_put": round(t_put, 4), "seconds_with_close": round(t_all, 4),
+                           "dir": os.path.abspath(a.dir)}
+                    print(json.dumps(row), flush=True)
+                    rows.append(row)
+                shutil.rmtree(db, ignore_errors=True)
         finally:
             shutil.rmtree(d, ignore_errors=True)
     if a.out:
