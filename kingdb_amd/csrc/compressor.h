@@ -114,6 +114,18 @@ class CompressorLZ4 {
   Status UncompressFrames(uint32_t n, char* const* frames, const uint64_t* frame_avail, char* const* out,
                           const uint64_t* out_cap, uint64_t* size_out);
 
+  // Bytes [offset, offset + size) of `whole` (a buffer of its own, offset 0),
+  // sharing its storage.  ByteArray's offset/size setters are private to its
+  // friends, this class among them (util/byte_array.h:184-192, 269-276): the
+  // flush hook hands each order a slice of one arena per GPU batch instead of
+  // a new[] buffer per order.
+  static ByteArray Slice(const ByteArray& whole, uint64_t offset, uint64_t size) {
+    ByteArray b = whole;
+    b.set_offset(offset);
+    b.set_size(size);
+    return b;
+  }
+
   // Reference quirk: Uncompress() always streams each frame
   // into crc32_ and UncompressByteArray() streams it again when verifying, so
   // verification of a compressed value fails.  true (default) = bug-for-bug.

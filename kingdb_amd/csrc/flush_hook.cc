@@ -24,6 +24,8 @@
 // IOError: the process keeps running.
 #include "cache/lz4_flush.h"
 
+#include "algorithm/compressor.h"
+
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -150,7 +152,9 @@ struct Intake {
 };
 
 struct Result {
-  ByteArray chunk_final;   // KDB_FLUSH_FRAME / KDB_FLUSH_DISABLED
+  ByteArray chunk_final;   // KDB_FLUSH_FRAME / KDB_FLUSH_DISABLED: a slice of the batch's arena
+  ByteArray raw;           // the raw chunk, held until the result is dropped by the worker, so
+                           // that completing an order never frees it on the flush thread
   uint64_t occ = 0, svc = 0;
   uint32_t crc = 0;
   uint8_t mode = KDB_FLUSH_RAW;
@@ -235,6 +239,7 @@ class Pipeline {
 
  private:
   void run();
+  void drop_consumed();
   void process(std::vector<Intake>& batch, uint64_t t0);
   int gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out);
 
@@ -251,7 +256,7 @@ class Pipeline {
   std::chrono::steady_clock::time_point intake_since_;
   uint64_t next_ticket_ = 1;
   uint64_t processed_ = 1;           // tickets below have results
-  bool drain_ = false, stop_ = false, failed_ = false;
+  bool drain_ = false, stop_ = false, failed_ = false, garbage_ = false;
   std::string failure_;
   // results (worker appends, flush thread consumes)
   std::mutex res_mu_;
@@ -275,6 +280,13 @@ void Pipeline::run() {
     {
       std::unique_lock<std::mutex> lk(mu_);
       for (;;) {
+        if (garbage_) {
+          garbage_ = false;
+          lk.unlock();
+          drop_consumed();
+          lk.lock();
+          continue;
+        }
         if (intake_.empty()) {
           if (drain_) {
             drain_ = false;
@@ -351,9 +363,12 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   std::vector<uint32_t> part_seg(m), seg_run, seg_head;   // seg_head: the segment's first entry
   std::vector<std::thread::id> run_tid;
   std::vector<kdb_flush_state> carry;
+  std::thread::id last_tid;
+  auto last_it = cur.end();
   for (uint32_t i = 0; i < m; i++) {
     const Intake& e = batch[i];
-    auto it = cur.find(e.tid);
+    // (consecutive parts mostly come from one thread: skip the hash lookup)
+    auto it = (last_it != cur.end() && e.tid == last_tid) ? last_it : cur.find(e.tid);
     const bool fresh = e.offset_chunk == 0;
     if (it == cur.end() || (fresh && e.chunk.size_const() > 0)) {
       const bool seen = it != cur.end();
@@ -369,7 +384,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
       seg_run.push_back(r);
       seg_head.push_back(i);
       if (seen) it->second = Cur{r, sg};
-      else cur.emplace(e.tid, Cur{r, sg});
+      else it = cur.emplace(e.tid, Cur{r, sg}).first;
       part_seg[i] = sg;
     } else if (fresh) {
       const uint32_t sg = (uint32_t)seg_run.size();
@@ -380,6 +395,8 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     } else {
       part_seg[i] = it->second.seg;
     }
+    last_tid = e.tid;
+    last_it = it;
   }
   const uint32_t nseg = (uint32_t)seg_run.size(), nruns = (uint32_t)run_tid.size();
   // order: segments grouped by run, parts grouped by segment (both stable)
@@ -483,8 +500,19 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   const double t_gpu_ms = ms_since(t_gpu);
   const Clock::time_point t_res = Clock::now();
   // ---- results, in ticket order
+  // one arena per batch: the packed frames, then the disabled-compression forms
   const kdb_flush_part* parts = reinterpret_cast<const kdb_flush_part*>(hb + h_out + p_parts);
   const kdb_flush_state* cout = reinterpret_cast<const kdb_flush_state*>(hb + h_out + p_carry);
+  uint64_t disabled_bytes = 0;
+  for (uint32_t q = 0; q < m; q++)
+    if (parts[q].status == 0 && parts[q].mode == KDB_FLUSH_DISABLED) disabled_bytes += parts[q].size;
+  ByteArray arena;
+  if (total + disabled_bytes) {
+    char* a = new char[total + disabled_bytes];
+    memcpy(a, hb + h_frames, total);
+    arena = NewShallowCopyByteArray(a, total + disabled_bytes);
+  }
+  uint64_t dis_at = total;
   for (uint32_t q = 0; q < m; q++) {
     const kdb_flush_part& P = parts[q];
     Intake& e = batch[perm[q]];
@@ -494,17 +522,17 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     r.crc = P.crc;
     r.mode = (uint8_t)P.mode;
     r.status = P.status == 0 ? 0 : -1;
+    r.raw = e.chunk;
     if (r.status) continue;
     if (P.mode == KDB_FLUSH_FRAME) {
       if (P.frame_at + P.size > total) return KDB_LZ4_EHIP;
-      char* b = new char[P.size];
-      memcpy(b, hb + h_frames + P.frame_at, P.size);
-      r.chunk_final = NewShallowCopyByteArray(b, P.size);
+      r.chunk_final = CompressorLZ4::Slice(arena, P.frame_at, P.size);
     } else if (P.mode == KDB_FLUSH_DISABLED) {             // database.cc:201-206
-      char* b = new char[P.size];
+      char* b = arena.data() + dis_at;
       memset(b, 0, 8);
       memcpy(b + 8, e.chunk.data(), P.size - 8);
-      r.chunk_final = NewShallowCopyByteArray(b, P.size);
+      r.chunk_final = CompressorLZ4::Slice(arena, dis_at, P.size);
+      dis_at += P.size;
     }
   }
   // each thread's state after its last run of the batch
@@ -565,7 +593,6 @@ void Pipeline::complete(std::vector<Order>& orders) {
     o.offset_chunk = r.occ;
     o.size_value_compressed = r.svc;
     o.crc32 = r.crc;
-    r.chunk_final = ByteArray();
   }
   if (dropped) {
     size_t w = 0;
@@ -580,13 +607,32 @@ void Pipeline::complete(std::vector<Order>& orders) {
   stats_.flushes++;
   stats_.orders += orders.size();
   stats_.complete_ms += ms_since(t0);
-  while (!res_.empty()) {
-    const uint32_t t = (uint32_t)res_base_;
-    auto c = cancelled_.find(t);
-    if (!res_.front().consumed && c == cancelled_.end()) break;
-    if (c != cancelled_.end()) cancelled_.erase(c);
-    res_.pop_front();
-    res_base_++;
+  // the consumed results are dropped by the worker (drop_consumed), off this thread
+  {
+    std::lock_guard<std::mutex> l2(mu_);
+    garbage_ = true;
+  }
+  cv_work_.notify_one();
+}
+
+// Worker: drops the consumed (or cancelled) results at the front, freeing
+// their buffers here rather than on the flush thread.
+void Pipeline::drop_consumed() {
+  std::deque<Result> dead;
+  {
+    std::lock_guard<std::mutex> l(res_mu_);
+    size_t k = 0;
+    while (k < res_.size()) {
+      const uint32_t t = (uint32_t)(res_base_ + k);
+      auto c = cancelled_.find(t);
+      if (!res_[k].consumed && c == cancelled_.end()) break;
+      if (c != cancelled_.end()) cancelled_.erase(c);
+      k++;
+    }
+    if (k == 0) return;
+    dead.insert(dead.end(), std::make_move_iterator(res_.begin()), std::make_move_iterator(res_.begin() + (long)k));
+    res_.erase(res_.begin(), res_.begin() + (long)k);
+    res_base_ += k;
   }
 }
 
