@@ -114,16 +114,27 @@ class CompressorLZ4 {
   Status UncompressFrames(uint32_t n, char* const* frames, const uint64_t* frame_avail, char* const* out,
                           const uint64_t* out_cap, uint64_t* size_out);
 
-  // Bytes [offset, offset + size) of `whole` (a buffer of its own, offset 0),
-  // sharing its storage.  ByteArray's offset/size setters are private to its
+  // Bytes [offset, offset + size) of `whole`'s view, sharing its storage.  ByteArray's offset/size setters are private to its
   // friends, this class among them (util/byte_array.h:184-192, 269-276): the
   // flush hook hands each order a slice of one arena per GPU batch instead of
   // a new[] buffer per order.
   static ByteArray Slice(const ByteArray& whole, uint64_t offset, uint64_t size) {
     ByteArray b = whole;
-    b.set_offset(offset);
+    b.increment_offset(offset);   // relative to whole's own view
     b.set_size(size);
+    b.set_size_compressed(0);
     return b;
+  }
+
+  // A stored value's fields the read hooks need (private to ByteArray's
+  // friends, like Slice): size, size_compressed, checksum, checksum_initial.
+  struct StoredView {
+    uint64_t size, size_compressed;
+    uint32_t checksum, checksum_initial;
+  };
+  static StoredView View(const ByteArray& v) {
+    ByteArray& w = const_cast<ByteArray&>(v);
+    return StoredView{w.size(), w.size_compressed(), w.checksum(), w.checksum_initial()};
   }
 
   // Reference quirk: Uncompress() always streams each frame

@@ -28,6 +28,62 @@ REF = os.environ.get("REF", "/root/reference")
 
 INCLUDE = '#include "cache/lz4_flush.h"\n'
 
+GETVALUE_OLD = """    // TODO-36: Uncompression should not have to go through a MultipartReader. See
+    //          the notes about this TODO in kingdb.cc.
+    char* buffer = new char[value_.size()];
+    uint64_t offset = 0;
+    MultipartReader mp_reader(read_options_, value_);
+    for (mp_reader.Begin(); mp_reader.IsValid(); mp_reader.Next()) {
+      ByteArray part;
+      mp_reader.GetPart(&part);
+      log::trace("ByteArray::GetValue()", "Multipart loop size:%d [%s]", part.size(), part.ToString().c_str());
+      memcpy(buffer + offset, part.data(), part.size());
+      offset += part.size();
+    }
+    status_ = mp_reader.GetStatus();
+    if (!status_.IsOK()) log::trace("ByteArray::GetValue()", "Error in GetValue(): %s\\n", status_.ToString().c_str());
+    return NewShallowCopyByteArray(buffer, value_.size());
+"""
+GETVALUE_NEW = """    // this value and the next entries' values, decoded in one GPU batch (LZ4ReadAhead)
+    return lz4_read_ahead_.Get(read_options_, value_, se_readonly_->db_options_.internal__size_multipart_required,
+                               &status_, [this](std::vector<ByteArray>* ahead) { LZ4PeekAhead(ahead); });
+"""
+REGULAR_PEEK = """  LZ4ReadAhead lz4_read_ahead_;
+  // the entries Next() will visit in the current HSTable (some may be skipped
+  // there as overwritten: decoding them is only wasted work)
+  void LZ4PeekAhead(std::vector<ByteArray>* ahead) {
+    for (uint32_t i = index_location_; i < locations_current_.size() && ahead->size() < LZ4ReadAhead::kMaxValues; i++) {
+      ByteArray key, value;
+      if (se_readonly_->GetEntry(read_options_, locations_current_[i], &key, &value).IsOK()) ahead->push_back(value);
+    }
+  }
+"""
+SEQUENTIAL_PEEK = """  LZ4ReadAhead lz4_read_ahead_;
+  // the entries Next() will visit in the current HSTable, decoded as Next() decodes them
+  void LZ4PeekAhead(std::vector<ByteArray>* ahead) {
+    if (!has_file_ || !mmap_.is_valid()) return;
+    uint64_t off = offset_;
+    while (off < offset_end_ && ahead->size() < LZ4ReadAhead::kMaxValues) {
+      struct EntryHeader h;
+      uint32_t hs;
+      Status s = EntryHeader::DecodeFrom(se_readonly_->db_options_, read_options_, mmap_.datafile() + off,
+                                         mmap_.filesize() - off, &h, &hs);
+      if (!s.IsOK() || !h.AreSizesValid(off, mmap_.filesize())) break;
+      ByteArray value = ByteArray::NewPooledByteArray(se_readonly_->file_manager_, fileid_current_,
+                                                      filepath_current_, mmap_.filesize_);
+      if (read_options_.verify_checksums)
+        value.set_checksum_initial(crc32c::Value(value.data() + off + hs, h.size_key));
+      value.set_offset(off + hs + h.size_key);
+      value.set_size(h.size_value);
+      value.set_size_compressed(h.size_value_compressed);
+      value.set_checksum(h.checksum_content);
+      ahead->push_back(value);
+      off += hs + h.size_key + h.size_value_offset();
+    }
+  }
+"""
+READ_INCLUDE = '#include "interface/lz4_read.h"\n'
+
 EDITS = {
     "interface/database.cc": [
         ('#include "interface/database.h"\n', '#include "interface/database.h"\n' + INCLUDE),
@@ -63,16 +119,45 @@ EDITS = {
          "    }\n"
          "    event_manager_->flush_buffer.StartAndBlockUntilDone(buffers_[im_copy_]);\n"),
     ],
+    # read side (INTEGRATION.md level 5): headers, so every translation unit of
+    # the hook build sees them (oracle/Makefile puts the copies first on the path)
+    "interface/iterator.h": [
+        ('#include "interface/multipart.h"\n', '#include "interface/multipart.h"\n' + READ_INCLUDE),
+        (GETVALUE_OLD, GETVALUE_NEW, 2),      # RegularIterator and SequentialIterator alike
+        ("  Status status_;\n\n  ByteArray key_;\n  ByteArray value_;\n};\n",
+         "  Status status_;\n\n  ByteArray key_;\n  ByteArray value_;\n" + REGULAR_PEEK + "};\n"),
+        ("  Mmap mmap_;\n\n  ByteArray key_;\n  ByteArray value_;\n};\n",
+         "  Mmap mmap_;\n\n  ByteArray key_;\n  ByteArray value_;\n" + SEQUENTIAL_PEEK + "};\n"),
+    ],
+    "interface/multipart.h": [
+        ('#include "interface/kingdb.h"\n', '#include "interface/kingdb.h"\n' + READ_INCLUDE),
+        ('    status_ = Status::IOError("Stream is unfinished");\n    Next();\n',
+         '    status_ = Status::IOError("Stream is unfinished");\n'
+         '    lz4_decode_.Prepare(read_options_, value_);   // all frames in one GPU launch\n'
+         '    Next();\n'),
+        ("  virtual bool Next() {\n    if (is_compressed() && !is_compression_disabled_) {\n",
+         "  virtual bool Next() {\n"
+         "    if (lz4_decode_.active()) {   // the parts Begin decoded\n"
+         "      lz4_decode_.Next(&chunk_, &status_, &is_valid_stream_);\n"
+         "      return true;\n"
+         "    }\n"
+         "    if (is_compressed() && !is_compression_disabled_) {\n"),
+        ("  ReadOptions read_options_;\n  ByteArray value_;\n};\n",
+         "  ReadOptions read_options_;\n  ByteArray value_;\n  LZ4MultipartDecode lz4_decode_;\n};\n"),
+    ],
 }
+
 
 
 def apply(out: str) -> None:
     for rel, edits in EDITS.items():
         with open(os.path.join(REF, rel)) as f:
             text = f.read()
-        for old, new in edits:
-            if text.count(old) != 1:
-                sys.exit(f"kingdb_hook: anchor found {text.count(old)} times in {rel}: {old!r}")
+        for e in edits:
+            old, new = e[0], e[1]
+            want = e[2] if len(e) > 2 else 1
+            if text.count(old) != want:
+                sys.exit(f"kingdb_hook: anchor found {text.count(old)} times (want {want}) in {rel}: {old!r}")
             text = text.replace(old, new)
         dst = os.path.join(out, rel)
         os.makedirs(os.path.dirname(dst), exist_ok=True)

@@ -33,10 +33,10 @@
 static bool rd(FILE* f, void* p, size_t n) { return n == 0 || fread(p, 1, n, f) == n; }
 
 // ref_db --verify <dbdir> <stream.bin> [options as above]: opens the database and reads every
-// key of the stream back (Database::Get, verify_checksums off -- the
+// key of the stream back three ways -- Database::Get (verify_checksums off: the
 // reference's double CRC stream fails it for compressed values, SURVEY.md
-// §0-7): prints "verify F found M missing", returns 1 if a value read back
-// differs from the last one put for its key.  (The fault-injection test of the
+// §0-7), the iterator's GetValue, and a MultipartReader per key -- and returns
+// 1 if any value read back differs from the last one put for its key.  (The fault-injection test of the
 // flush hook: no entry reaches an HSTable without its frame and checksum.)
 static int verify(int argc, char** argv) {
   const char *dir = argv[2], *stream = argv[3];
@@ -88,10 +88,38 @@ static int verify(int argc, char** argv) {
       found++;
     }
   }
+  // the same values through the iterator (GetValue) and MultipartReader
+  uint64_t it_items = 0, it_bad = 0, mp_bad = 0;
+  {
+    kdb::Iterator it = db.NewIterator(ro);
+    for (it.Begin(); it.IsValid(); it.Next()) {
+      kdb::ByteArray k = it.GetKey(), v = it.GetValue();
+      it_items++;
+      auto f = last.find(k.ToString());
+      if (f == last.end() || !it.GetStatus().IsOK() || v.ToString() != f->second) {
+        if (it_bad++ < 5) fprintf(stderr, "iterator key %s: %s\n", k.ToString().c_str(), it.GetStatus().ToString().c_str());
+      }
+    }
+  }
+  for (auto& p : last) {
+    std::string probe;
+    if (!db.Get(ro, p.first, &probe).IsOK()) continue;   // (missing: counted above)
+    kdb::MultipartReader mp = db.NewMultipartReader(ro, p.first);
+    std::string out;
+    for (mp.Begin(); mp.IsValid(); mp.Next()) {   // (a part's status is the stream's: "unfinished" mid-way)
+      kdb::ByteArray part;
+      mp.GetPart(&part);
+      out += part.ToString();
+    }
+    if (!mp.GetStatus().IsOK() || out != p.second) {
+      if (mp_bad++ < 5) fprintf(stderr, "multipart key %s: %s\n", p.first.c_str(), mp.GetStatus().ToString().c_str());
+    }
+  }
   db.Close();
-  printf("verify %llu found %llu missing %llu bad\n", (unsigned long long)found, (unsigned long long)missing,
-         (unsigned long long)bad);
-  return bad ? 1 : 0;
+  printf("verify %llu found %llu missing %llu bad %llu iterated %llu iterator_bad %llu multipart_bad\n",
+         (unsigned long long)found, (unsigned long long)missing, (unsigned long long)bad,
+         (unsigned long long)it_items, (unsigned long long)it_bad, (unsigned long long)mp_bad);
+  return bad || it_bad || mp_bad ? 1 : 0;
 }
 
 int main(int argc, char** argv) {

@@ -215,3 +215,50 @@ def test_hook_permanent_gpu_failure_is_survived(tmp_path, gpu, first):
     print(v.stdout.strip())
     if first == 1:
         assert found == 0
+
+
+def _verify(exe, db, stream, opts):
+    hs, ht, mps = opts
+    return subprocess.run([exe, "--verify", str(db), str(stream), str(mps), str(hs), str(ht)], capture_output=True,
+                          text=True, timeout=300)
+
+
+@pytest.mark.parametrize("name", ["small", "edge", "murmur", "multipart"])
+def test_hook_read_path_matches_reference_reads(tmp_path, gpu, name):
+    """The read hooks (INTEGRATION.md level 5): the hook build reads a database
+    back three ways -- Database::Get, the iterator's GetValue (LZ4ReadAhead: the
+    next entries decoded in one GPU batch) and MultipartReader (LZ4MultipartDecode:
+    all frames of a value in one launch) -- and every value equals the one put,
+    with the same found / missing / iterated counts as the reference build
+    reading the reference's own files."""
+    z, _ = _golden_streams()
+    opts = tuple(int(x) for x in z[f"{name}__opts"])
+    (tmp_path / "s.bin").write_bytes(z[f"{name}__stream"].tobytes())
+    r = _run_stream(_bin(REF, "kdb_db"), tmp_path / "ref", tmp_path / "s.bin", opts)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = _verify(_bin(REF, "kdb_db"), tmp_path / "ref", tmp_path / "s.bin", opts)
+    assert want.returncode == 0, want.stdout + want.stderr[-2000:]
+    r = _run_stream(_bin(HOOK, "kdb_db"), tmp_path / "hook", tmp_path / "s.bin", opts)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = _verify(_bin(HOOK, "kdb_db"), tmp_path / "hook", tmp_path / "s.bin", opts)
+    assert got.returncode == 0, got.stdout + got.stderr[-2000:]
+    assert got.stdout.split() == want.stdout.split()
+
+
+def test_hook_client_embedded_iteration_vs_reference(tmp_path, gpu):
+    """unit-tests/client_embedded.cc (1 M puts of 16 B keys / 100 B values, then
+    one iteration with GetValue) through the reference build and through the
+    hook build, on the same box in the same test: all items back in both, and
+    the times are printed (the read hooks' claim is the hook build's iteration
+    <= the reference's)."""
+    out = {}
+    for b, d in (("reference", REF), ("hook", HOOK)):
+        wd = tmp_path / b
+        wd.mkdir()
+        r = subprocess.run([_bin(d, "client_emb")], cwd=wd, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "count items: 1000000" in r.stdout
+        it = re.search(r"iteration done in (\d+) ms", r.stdout)
+        out[b] = int(it.group(1))
+        print(b, r.stdout.strip().replace("\n", " | "))
+    print("iteration ms", out)
