@@ -183,8 +183,12 @@ bool LZ4DecodeValues(std::vector<ByteArray>& values, bool verify, std::vector<By
 // ------------------------------------------------------------- LZ4ReadAhead
 ByteArray LZ4ReadAhead::Get(const ReadOptions& read_options, ByteArray& value, uint64_t max_size, Status* status,
                             const Peek& peek) {
-  auto it = cache_.find(value.data());
-  if (it == cache_.end() || it->second.out.size() != value.size()) {
+  // the iterator asks in order: the expected value, or one a little further
+  // on (entries Next() skipped); anything else starts a new batch
+  const char* key = value.data();
+  size_t i = cursor_;
+  while (i < batch_.size() && i < cursor_ + 64 && batch_[i].stored != key) i++;
+  if (i >= batch_.size() || batch_[i].stored != key || batch_[i].out.size() != value.size()) {
     std::vector<ByteArray> batch;
     batch.push_back(value);
     std::vector<ByteArray> ahead;
@@ -193,20 +197,22 @@ ByteArray LZ4ReadAhead::Get(const ReadOptions& read_options, ByteArray& value, u
     for (ByteArray& v : ahead) {
       if (batch.size() >= kMaxValues || bytes >= kMaxBytes) break;
       const uint64_t svc = CompressorLZ4::View(v).size_compressed;
-      if (svc == 0 || v.size() > max_size || cache_.count(v.data())) continue;
+      if (svc == 0 || v.size() > max_size) continue;
       batch.push_back(v);
       bytes += svc;
     }
     std::vector<ByteArray> out;
     std::vector<Status> st;
     LZ4DecodeValues(batch, read_options.verify_checksums, &out, &st);
-    cache_.clear();   // the previous batch's values are behind the iterator
-    for (size_t i = 0; i < batch.size(); i++) cache_[batch[i].data()] = Decoded{out[i], st[i]};
-    it = cache_.find(value.data());
+    batch_.clear();
+    batch_.reserve(batch.size());
+    for (size_t j = 0; j < batch.size(); j++) batch_.push_back(Decoded{batch[j].data(), out[j], st[j]});
+    i = 0;
   }
-  *status = it->second.st;
-  ByteArray r = it->second.out;
-  cache_.erase(it);
+  cursor_ = i + 1;
+  *status = batch_[i].st;
+  ByteArray r = batch_[i].out;
+  batch_[i].out = ByteArray();
   return r;
 }
 

@@ -24,7 +24,6 @@
 
 #include <cstdint>
 #include <functional>
-#include <unordered_map>
 #include <vector>
 
 #include "util/byte_array.h"
@@ -51,10 +50,12 @@ class LZ4ReadAhead {
 
  private:
   struct Decoded {
+    const char* stored;   // the value's stored bytes (its identity while the batch lives)
     ByteArray out;
     Status st;
   };
-  std::unordered_map<const char*, Decoded> cache_;   // by the value's stored bytes
+  std::vector<Decoded> batch_;   // in iteration order
+  size_t cursor_ = 0;            // the next value GetValue is expected to ask for
 };
 
 class LZ4MultipartDecode {

@@ -50,11 +50,36 @@ GETVALUE_NEW = """    // this value and the next entries' values, decoded in one
 """
 REGULAR_PEEK = """  LZ4ReadAhead lz4_read_ahead_;
   // the entries Next() will visit in the current HSTable (some may be skipped
-  // there as overwritten: decoding them is only wasted work)
+  // there as overwritten: decoding them is only wasted work); after the first
+  // (StorageEngine::GetEntry, storage_engine.h:459-521) the headers are decoded
+  // straight from the same pooled mapping of the file
   void LZ4PeekAhead(std::vector<ByteArray>* ahead) {
+    ByteArray file;
     for (uint32_t i = index_location_; i < locations_current_.size() && ahead->size() < LZ4ReadAhead::kMaxValues; i++) {
-      ByteArray key, value;
-      if (se_readonly_->GetEntry(read_options_, locations_current_[i], &key, &value).IsOK()) ahead->push_back(value);
+      const uint64_t location = locations_current_[i];
+      if (!file.resource_) {
+        ByteArray key, value;
+        if (!se_readonly_->GetEntry(read_options_, location, &key, &value).IsOK()) continue;
+        ahead->push_back(value);
+        file = value;
+        continue;
+      }
+      const uint32_t off = (uint32_t)(location & 0xFFFFFFFF);
+      const uint64_t filesize = file.resource_->size();
+      const char* base = file.resource_->data();
+      struct EntryHeader h;
+      uint32_t hs;
+      if (off >= filesize ||
+          !EntryHeader::DecodeFrom(se_readonly_->db_options_, read_options_, base + off, filesize - off, &h, &hs).IsOK() ||
+          !h.AreSizesValid(off, filesize) || !h.IsEntryFull() || h.IsTypeDelete())
+        continue;
+      ByteArray value = file;
+      if (read_options_.verify_checksums) value.set_checksum_initial(crc32c::Value(base + off + hs, h.size_key));
+      value.set_offset(off + hs + h.size_key);
+      value.set_size(h.size_value);
+      value.set_size_compressed(h.size_value_compressed);
+      value.set_checksum(h.checksum_content);
+      ahead->push_back(value);
     }
   }
 """

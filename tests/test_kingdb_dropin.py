@@ -255,7 +255,11 @@ def test_hook_client_embedded_iteration_vs_reference(tmp_path, gpu):
     for b, d in (("reference", REF), ("hook", HOOK)):
         wd = tmp_path / b
         wd.mkdir()
-        r = subprocess.run([_bin(d, "client_emb")], cwd=wd, capture_output=True, text=True, timeout=600)
+        r = subprocess.run([_bin(d, "client_emb")], cwd=wd, capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, KDB_LZ4_FLUSH_STATS="1"))
+        for ln in r.stderr.splitlines():
+            if ln.startswith("lz4_flush_stats"):
+                print(b, ln)
         assert r.returncode == 0, r.stderr[-2000:]
         assert "count items: 1000000" in r.stdout
         it = re.search(r"iteration done in (\d+) ms", r.stdout)
