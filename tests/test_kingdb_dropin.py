@@ -266,3 +266,14 @@ def test_hook_client_embedded_iteration_vs_reference(tmp_path, gpu):
         out[b] = int(it.group(1))
         print(b, r.stdout.strip().replace("\n", " | "))
     print("iteration ms", out)
+
+
+def test_hook_concurrent_writers_and_readers(tmp_path, gpu):
+    """oracle/hook_mt.cc on the GPU build: 8 client threads put single-part and
+    multipart values at once (the flush pipeline carries each thread's
+    PutPartValidSize state), then 8 readers (Get, MultipartReader) and an
+    iteration get every value back byte for byte."""
+    r = subprocess.run([_bin(HOOK, "hook_mt"), str(tmp_path / "db"), "8", "150"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.startswith("ok:"), r.stdout
