@@ -76,6 +76,21 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def host_threads() -> tuple:
+    """Threads for a CPU leg and how they were chosen: every core the process
+    affinity allows, capped by OMP_NUM_THREADS where that is set -- on the GPU
+    box the harness sets it to the lease's CPU share (16 per GPU) while nproc and
+    the affinity mask show the whole machine, and worker pools are to be sized to
+    the share."""
+    nproc = os.cpu_count() or 1
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    cap_env = os.environ.get("OMP_NUM_THREADS")
+    cap = int(cap_env) if cap_env and cap_env.isdigit() and int(cap_env) > 0 else None
+    threads = max(1, min(affinity, cap) if cap else affinity)
+    return threads, {"nproc": nproc, "affinity": affinity, "cap": cap,
+                     "cap_source": "OMP_NUM_THREADS (the lease's CPU share)" if cap else None, "threads": threads}
+
+
 def cpu_baseline(sample: np.ndarray, size: int, seconds: float) -> dict:
     """Times the reference's algorithm/lz4.cc (oracle/_ref, kind "reference")
     or, where that build is absent, the oracle restatement (kind "port") on the
@@ -92,8 +107,7 @@ def cpu_baseline(sample: np.ndarray, size: int, seconds: float) -> dict:
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                    ctypes.POINTER(ctypes.c_uint64)]
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    threads, host = host_threads()
 
     def run(n, th, passes):
         tc, td, cb = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
@@ -112,7 +126,8 @@ def cpu_baseline(sample: np.ndarray, size: int, seconds: float) -> dict:
         res[label] = dict(rt=raw / (tc + td) / GIB, c=raw / tc / GIB, d=raw / td / GIB, n=n, passes=passes)
     a, o = res["all"], res["one"]
     return {
-        "value": round(a["rt"], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "value": round(a["rt"], 3), "unit": "GiB/s", "cores": threads, "kind": kind, "host": host,
+        "per_core_gibs": round(a["rt"] / threads, 3),
         "sample": (f"{a['n']} x {size} B G1-long values (the first values of the GPU batch), "
                    f"{a['passes']} timed round-trip passes after 1 warm-up, blocked partition over "
                    f"{threads} threads; CPU: {cpu_model()}"),
@@ -139,8 +154,7 @@ def cpu_baseline_mixed(sample: np.ndarray, off: np.ndarray, lens: np.ndarray, se
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                    ctypes.POINTER(ctypes.c_uint64)]
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    threads, host = host_threads()
     off = np.ascontiguousarray(off, np.uint64)
     lens = np.ascontiguousarray(lens, np.uint32)
 
@@ -162,7 +176,8 @@ def cpu_baseline_mixed(sample: np.ndarray, off: np.ndarray, lens: np.ndarray, se
         res[label] = dict(rt=raw / (tc + td) / GIB, c=raw / tc / GIB, d=raw / td / GIB, n=n, passes=passes)
     a, o = res["all"], res["one"]
     return {
-        "value": round(a["rt"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference",
+        "value": round(a["rt"], 3), "unit": "GiB/s", "cores": threads, "kind": "reference", "host": host,
+        "per_core_gibs": round(a["rt"] / threads, 3),
         "sample": (f"the first {a['n']} values of the mixed batch ({int(lens.astype(np.int64).sum())} B), "
                    f"{a['passes']} timed round-trip passes after 1 warm-up, byte-balanced over {threads} threads; "
                    f"CPU: {cpu_model()}"),
@@ -226,6 +241,8 @@ def host_inclusive(batch, n: int, size: int, args) -> dict:
         "chunk": hp.chunk, "streams": len(hp.streams),
         "timing": "host wall clock, first enqueue to last byte in pinned host memory; median of 3 after 1 warm-up",
     }
+    # where the wall time goes (traced runs after the timed ones; weak #9 of round 2)
+    res["stall_profile"] = hp.profile()
     hp.free()
     return res
 
@@ -304,8 +321,7 @@ def ref_read_path(stored: np.ndarray, off: np.ndarray, lens: np.ndarray, size: i
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int,
                    ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = max(1, min(avail, int(os.environ.get("OMP_NUM_THREADS", avail))))
+    threads, host = host_threads()
     n = len(lens)
     off = np.ascontiguousarray(off, np.uint64)
     lens = np.ascontiguousarray(lens, np.uint64)
@@ -316,7 +332,7 @@ def ref_read_path(stored: np.ndarray, off: np.ndarray, lens: np.ndarray, size: i
     if fn(stored.ctypes.data, off.ctypes.data, lens.ctypes.data, n, size, threads, passes, ctypes.byref(t)) != 0:
         raise RuntimeError("reference read path failed on the sample")
     return {"value": round(float(n) * size * passes / t.value / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "reference",
+            "kind": "reference", "host": host,
             "sample": f"{n} stored {size} B G1-long values (the first of the GPU batch), {passes} timed passes after "
                       f"1 warm-up, blocked over {threads} threads; CPU: {cpu_model()}",
             "source": "algorithm/compressor.cc CompressorLZ4::UncompressByteArray (verify off), compiled from the "
@@ -567,11 +583,16 @@ def main() -> None:
     barrier()
     sync_all()
     t0 = time.perf_counter()
+    names = {}
     for k in range(args.steps):
         evs[k][0].record(stream)
         batch.compress(stream)
+        if k == 0:
+            names["compress"] = L.last_kernels()    # host-side record of what was queued, no HIP call
         evs[k][1].record(stream)
         batch.decompress(stream)
+        if k == 0:
+            names["decompress"] = L.last_kernels()
         evs[k][2].record(stream)
     stream.sync()
     sync_all()
@@ -594,34 +615,41 @@ def main() -> None:
     raw = float(batch.raw_bytes)
     frames = float(flen.sum())
     alg_bytes = raw + frames  # per launch, compress and decompress alike
-    if args.workload == "mixed":
-        # several size-class launches per step: the roofline covers the step's launches together
-        kc, kd = "all compress launches of the step", "all decompress launches of the step"
-    else:
-        # the launch a uniform batch of this size gets (launch_compress / launch_decompress)
-        kc = ("kdb_lz4::lz4_compress_kernel<true, true>" if size <= 4096 else
-              "kdb_lz4::lz4_compress_mixed_kernel<true>" if size < 65547 else
-              "kdb_lz4::lz4_compress_big_kernel<true, true>")
-        kd = "kdb_lz4::lz4_decompress_kernel<true>" if size <= 8192 else "kdb_lz4::lz4_decompress_mixed_kernel<true>"
+    # the kernels the step's launches actually queued (kdb_lz4_last_kernels): a
+    # mixed step has one launch per size class, covered by the roofline together
+    kc = " + ".join(names["compress"])
+    kd = " + ".join(names["decompress"])
     if c_ms >= d_ms:
         dom_key, dom_name, dom_ms = "compress", kc, c_ms
     else:
         dom_key, dom_name, dom_ms = "decompress", kd, d_ms
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     # HBM bytes of the same launch(es) from committed PMC passes of this exact
-    # workload (tools/pmc_traffic.py); traffic_source names the file and its passes
-    traffic, traffic_source = None, None
+    # workload (tools/pmc_traffic.py); used only when the passes were taken with
+    # this very build (kdb_lz4_build_id) and name the kernels this run queued
+    traffic, traffic_source, traffic_refused = None, None, None
     pmc = args.pmc or os.path.join(ROOT, "profiles",
                                    "pmc_traffic_mixed.json" if args.workload == "mixed" else "pmc_traffic.json")
     try:
         pm = json.load(open(pmc))
         want = (args.values, "mixed") if args.workload == "mixed" else (n, size)
-        if (pm.get("values"), pm.get("size")) == want and (world == 1 or args.workload == "uniform"):
-            traffic = pm["kernels"][dom_key]["hbm_bytes_per_launch"]
+        got = pm["kernels"][dom_key]
+        got_names = set(k.replace("kdb_lz4::", "") for k in (got.get("kernel") or "").split(" + "))
+        if (pm.get("values"), pm.get("size")) != want or not (world == 1 or args.workload == "uniform"):
+            traffic_refused = "no PMC passes of this workload"
+        elif pm.get("build_id") != L.build_id():
+            traffic_refused = (f"PMC passes taken with build {pm.get('build_id')}, this run uses {L.build_id()}")
+        elif args.workload == "uniform" and not got_names <= set(names[dom_key]):
+            traffic_refused = f"PMC kernel {sorted(got_names)} not among this run's {names[dom_key]}"
+        elif args.workload == "mixed" and got_names != set(names[dom_key]):
+            traffic_refused = f"PMC kernels {sorted(got_names)} differ from this run's {names[dom_key]}"
+        else:
+            traffic = got["hbm_bytes_per_launch"]
             traffic_source = {"file": os.path.relpath(pmc, ROOT), "passes": pm.get("passes"),
+                              "build_id": pm.get("build_id"),
                               "scope": pm.get("scope", "the kind's dominant launch")}
-    except (OSError, ValueError, KeyError):
-        pass
+    except (OSError, ValueError, KeyError) as e:
+        traffic_refused = f"no usable PMC summary ({type(e).__name__})"
 
     total_raw = max_over_ranks(raw, op="sum") * args.steps
     value = total_raw / elapsed / GIB
@@ -655,6 +683,7 @@ def main() -> None:
             "bound": "hbm", "kernel": dom_name,
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": traffic_source,
+            "traffic_refused": traffic_refused, "build_id": L.build_id(),
             "alg_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(dom_ms, 4),
             "copy_gbs": round(copy_gbs, 1), "frac_of_copy": round(achieved / copy_gbs, 5),
         },

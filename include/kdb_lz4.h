@@ -56,6 +56,10 @@ int kdb_lz4_warmup(void);
 /* The kernels (rocprof names, ';'-separated) that the calling thread's last
  * compress or decompress batch queued.  No HIP call. */
 int kdb_lz4_last_kernels(char* buf, uint64_t cap);
+/* The build id of the loaded library: a hash of the HIP and header sources it
+ * was compiled from (kingdb_amd/Makefile), so that measurements taken with one
+ * build (e.g. committed PMC traffic) can be matched to the build in use. */
+int kdb_lz4_build_id(char* buf, uint64_t cap);
 int kdb_lz4_malloc(void** ptr, uint64_t bytes);              /* device memory */
 int kdb_lz4_free(void* ptr);
 int kdb_lz4_host_alloc(void** ptr, uint64_t bytes);          /* pinned host memory */

@@ -12,6 +12,7 @@ from .lz4 import (  # noqa: F401
     Stream,
     compress_blocks,
     compress_bound,
+    build_id,
     compress_frames,
     compress_limited_output,
     decompress_blocks,
@@ -26,7 +27,7 @@ from .lz4 import (  # noqa: F401
 )
 
 __all__ = [
-    "DeviceBatch", "DeviceBuffer", "Event", "Stream", "compress_blocks", "compress_bound",
+    "DeviceBatch", "DeviceBuffer", "Event", "Stream", "build_id", "compress_blocks", "compress_bound",
     "compress_frames", "compress_limited_output", "decompress_blocks", "decompress_frames",
     "decompress_safe_partial", "device_count", "frame_bound", "get_device", "last_kernels", "selftest",
     "set_device",

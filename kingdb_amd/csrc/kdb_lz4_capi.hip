@@ -236,6 +236,17 @@ int kdb_lz4_last_kernels(char* buf, uint64_t cap) {
   buf[k] = 0;
   return KDB_LZ4_OK;
 }
+#ifndef KDB_BUILD_ID
+#define KDB_BUILD_ID "unstamped"
+#endif
+int kdb_lz4_build_id(char* buf, uint64_t cap) {
+  if (!buf || cap == 0) return KDB_LZ4_EINVAL;
+  const size_t n = strlen(KDB_BUILD_ID);
+  const size_t k = n < cap - 1 ? n : (size_t)cap - 1;
+  memcpy(buf, KDB_BUILD_ID, k);
+  buf[k] = 0;
+  return KDB_LZ4_OK;
+}
 int kdb_lz4_get_device(int* device) { return device ? hip_status(hipGetDevice(device)) : KDB_LZ4_EINVAL; }
 int kdb_lz4_malloc(void** ptr, uint64_t bytes) {
   return ptr ? hip_status(hipMalloc(ptr, bytes ? bytes : 1)) : KDB_LZ4_EINVAL;

@@ -65,6 +65,13 @@ __device__ __forceinline__ int first_zero_or_neg(uint64_t m) {
   asm("s_ff0_i32_b64 %0, %1" : "=s"(r) : "s"(m));
   return r;
 }
+// One s_flbit_i32_b64: the number of zero bits above the highest set bit of
+// m (lanes 63, 62, ... before the first set one), -1 if m is 0.
+__device__ __forceinline__ int leading_zeros_or_neg(uint64_t m) {
+  int r;
+  asm("s_flbit_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+  return r;
+}
 
 // Dynamic work distribution of the persistent kernels.  Lane 0 claims `batch`
 // consecutive value indices with one device-scope atomic.  A single counter

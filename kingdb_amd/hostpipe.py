@@ -32,6 +32,19 @@ from . import _lib
 from .lz4 import DeviceBuffer, Event, Stream, frame_bound, lib
 
 
+def _union(ivs) -> float:
+    """Total length of the union of [a, b) intervals."""
+    tot, end = 0.0, None
+    for a, b in sorted(ivs):
+        if end is None or a > end:
+            tot += b - a
+            end = b
+        elif b > end:
+            tot += b - end
+            end = b
+    return tot
+
+
 class PinnedBuffer:
     """hipHostMalloc'd bytes with a numpy view."""
 
@@ -96,6 +109,18 @@ class HostPipeline:
         self.d_dconst.upload(dc)
         self.frame_bytes = 0
         self.frame_off = np.zeros(n + 1, np.uint64)
+        self._trace = None        # [(kind, chunk, start Event, end Event)] while profile() runs
+
+    def _mark(self, st) -> "Event | None":
+        if self._trace is None:
+            return None
+        e = Event()
+        e.record(st)
+        return e
+
+    def _span(self, kind: str, c: int, e0, st) -> None:
+        if self._trace is not None:
+            self._trace.append((kind, c, e0, self._mark(st)))
 
     def _range(self, c: int) -> tuple[int, int]:
         lo = c * self.chunk
@@ -116,8 +141,10 @@ class HostPipeline:
             st = self.streams[c % S].ptr
             _lib.check(L.kdb_lz4_event_sync(done[c].ptr), "event_sync")
             tot = int(self.h_tot.np[8 * c: 8 * c + 8].view(np.uint64)[0])
+            e0 = self._mark(self.streams[c % S])
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_frames.ptr + host_off, self.d_packed.ptr + lo * self.slot,
                                             tot, st), "d2h frames")
+            self._span("d2h", c, e0, self.streams[c % S])
             chunk_off[c] = host_off
             host_off += tot
 
@@ -127,10 +154,13 @@ class HostPipeline:
             m = hi - lo
             st = self.streams[c % S].ptr
             cm, dm = self.h_cmeta.ptr, self.d_cmeta.ptr
+            e0 = self._mark(self.streams[c % S])
             for base, w in ((0, 8), (8 * n, 4), (12 * n, 8)):
                 _lib.check(L.kdb_lz4_memcpy_h2d(dm + base + w * lo, cm + base + w * lo, w * m, st), "h2d meta")
             _lib.check(L.kdb_lz4_memcpy_h2d(self.d_raw.ptr + lo * size, self.h_raw.ptr + lo * size, m * size, st),
                        "h2d raw")
+            self._span("h2d", c, e0, self.streams[c % S])
+            e0 = self._mark(self.streams[c % S])
             flen = self.d_cres.ptr + 4 * lo
             stat = self.d_cres.ptr + 4 * n + 4 * lo
             _lib.check(L.kdb_lz4_compress_frames_batch(
@@ -139,6 +169,7 @@ class HostPipeline:
             _lib.check(L.kdb_lz4_pack_frames(
                 st, self.d_slots.ptr, dm + 12 * n + 8 * lo, flen, m, self.d_packed.ptr + lo * self.slot,
                 self.d_pack_off.ptr + 8 * lo, self.d_tot.ptr + 8 * c), "pack_frames")
+            self._span("kernel", c, e0, self.streams[c % S])
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_tot.ptr + 8 * c, self.d_tot.ptr + 8 * c, 8, st), "d2h total")
             done[c].record(self.streams[c % S])
             for base in (4 * lo, 4 * n + 4 * lo):
@@ -181,24 +212,91 @@ class HostPipeline:
             m = hi - lo
             st = self.streams[c % S].ptr
             f0, f1 = int(self.frame_off[lo]), int(self.frame_off[hi])
+            e0 = self._mark(self.streams[c % S])
             _lib.check(L.kdb_lz4_memcpy_h2d(self.d_packed.ptr + f0, self.h_frames.ptr + f0, f1 - f0, st), "h2d frames")
             for base, w in ((0, 8), (8 * n, 4)):
                 _lib.check(L.kdb_lz4_memcpy_h2d(self.d_dmeta.ptr + base + w * lo, self.h_dmeta.ptr + base + w * lo,
                                                 w * m, st), "h2d meta")
+            self._span("h2d", c, e0, self.streams[c % S])
+            e0 = self._mark(self.streams[c % S])
             olen = self.d_dres.ptr + 4 * lo
             stat = self.d_dres.ptr + 4 * n + 4 * lo
             _lib.check(L.kdb_lz4_decompress_frames_batch(
                 st, self.d_packed.ptr, self.d_dmeta.ptr + 8 * lo, self.d_dmeta.ptr + 8 * n + 4 * lo, m, max_in, size,
                 self.d_out.ptr, self.d_dconst.ptr + 8 * lo, self.d_dconst.ptr + 8 * n + 4 * lo, olen, stat),
                 "decompress_frames_batch")
+            self._span("kernel", c, e0, self.streams[c % S])
+            e0 = self._mark(self.streams[c % S])
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_out.ptr + lo * size, self.d_out.ptr + lo * size, m * size, st),
                        "d2h out")
+            self._span("d2h", c, e0, self.streams[c % S])
             for base in (4 * lo, 4 * n + 4 * lo):
                 _lib.check(L.kdb_lz4_memcpy_d2h(self.h_dres.ptr + base, self.d_dres.ptr + base, 4 * m, st),
                            "d2h results")
         for s in self.streams:
             s.sync()
         return time.perf_counter() - t0
+
+    def _copies(self, h2d: bool, d2h: bool) -> float:
+        """The link alone: n*size bytes in the pipeline's chunks over its
+        streams, one or both directions at once.  Wall seconds."""
+        L = lib()
+        S = len(self.streams)
+        t0 = time.perf_counter()
+        for c in range(self.nchunks):
+            lo, hi = self._range(c)
+            nb = (hi - lo) * self.size
+            if h2d:
+                _lib.check(L.kdb_lz4_memcpy_h2d(self.d_raw.ptr + lo * self.size, self.h_raw.ptr + lo * self.size, nb,
+                                                self.streams[c % S].ptr), "h2d")
+            if d2h:
+                _lib.check(L.kdb_lz4_memcpy_d2h(self.h_out.ptr + lo * self.size, self.d_out.ptr + lo * self.size, nb,
+                                                self.streams[(c + S // 2) % S].ptr), "d2h")
+        for s in self.streams:
+            s.sync()
+        return time.perf_counter() - t0
+
+    def profile(self) -> dict:
+        """Where the host-inclusive time goes: one traced compress and one
+        traced decompress (HIP events around every chunk's H2D, kernels and
+        D2H on its stream), each kind's busy time as the union of its
+        intervals, against the wall time and against the link alone (the same
+        bytes copied with no kernel, each direction and both at once)."""
+        raw = float(self.n) * self.size
+        link = {}
+        for name, h, d in (("h2d", True, False), ("d2h", False, True), ("both", True, True)):
+            self._copies(h, d)
+            t = min(self._copies(h, d) for _ in range(3))
+            link[name + "_gbs"] = round((raw * (h + d)) / t / 1e9, 2)
+        out = {"link_alone": link}
+        for phase in ("compress", "decompress"):
+            self._trace = []
+            base = Event()
+            base.record(self.streams[0])
+            wall = getattr(self, phase)()
+            spans, self._trace = self._trace, None
+            iv = {}
+            for kind, _c, e0, e1 in spans:
+                iv.setdefault(kind, []).append((base.elapsed_ms(e0), base.elapsed_ms(e1)))
+            res = {"wall_ms": round(wall * 1e3, 3)}
+            allcopy = []
+            for kind, ivs in sorted(iv.items()):
+                res[kind + "_busy_ms"] = round(_union(ivs), 3)
+                res[kind + "_sum_ms"] = round(sum(b - a for a, b in ivs), 3)
+                if kind != "kernel":
+                    allcopy += ivs
+            res["link_busy_ms"] = round(_union(allcopy), 3)
+            first = min(a for ivs in iv.values() for a, _ in ivs)
+            last = max(b for ivs in iv.values() for _, b in ivs)
+            res["device_span_ms"] = round(last - first, 3)
+            res["first_op_at_ms"] = round(first, 3)
+            out[phase] = res
+        by = {"compress": (raw, float(self.frame_bytes)), "decompress": (float(self.frame_bytes), raw)}
+        for phase, (hb, db) in by.items():
+            r = out[phase]
+            r["h2d_gbs_while_busy"] = round(hb / (r["h2d_busy_ms"] * 1e-3) / 1e9, 2)
+            r["d2h_gbs_while_busy"] = round(db / (r["d2h_busy_ms"] * 1e-3) / 1e9, 2)
+        return out
 
     def free(self) -> None:
         for b in (self.h_raw, self.h_frames, self.h_out, self.h_cmeta, self.h_cres, self.h_dmeta, self.h_dres,

@@ -64,6 +64,13 @@ def last_kernels() -> list:
     return [k for k in buf.value.decode().split(";") if k]
 
 
+def build_id() -> str:
+    """Hash of the sources the loaded library was compiled from (kdb_lz4_build_id)."""
+    buf = ctypes.create_string_buffer(64)
+    _lib.check(lib().kdb_lz4_build_id(buf, len(buf)), "build_id")
+    return buf.value.decode()
+
+
 # ------------------------------------------------------------ device memory
 class DeviceBuffer:
     """A hipMalloc'd byte range owned by Python."""

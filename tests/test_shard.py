@@ -119,7 +119,9 @@ def _gpu_worker(rank, world, port, out_dir):
     import oracle
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    K.set_device(rank % K.device_count())
+    want = rank % K.device_count()
+    K.set_device(want)
+    bound = [K.get_device()]           # the device this rank asked for, as the library sees it
     orc = oracle.Oracle()
     pool = oracle.g1_pool(orc)
     values = oracle.g1_values(pool, 100, 3000) + oracle.g1_values(pool, 4096, 300) + \
@@ -127,6 +129,7 @@ def _gpu_worker(rank, world, port, out_dir):
     lo, hi = byte_balanced_ranges([len(v) for v in values], world)[rank]
     frames = K.compress_frames(values[lo:hi])
     back = K.decompress_frames(frames, [len(v) for v in values[lo:hi]])
+    bound.append(K.get_device())       # and still bound after the batches
     ok = all(st == 0 and out == v for (st, out), v in zip(back, values[lo:hi]))
     mine = b"".join(frames)
     totals = [None] * world
@@ -135,7 +138,7 @@ def _gpu_worker(rank, world, port, out_dir):
     with open(os.path.join(out_dir, f"rank{rank}.bin"), "wb") as f:
         f.write(mine)
     with open(os.path.join(out_dir, f"rank{rank}.txt"), "w") as f:
-        f.write(f"{off} {int(ok)} {lo} {hi}")
+        f.write(f"{off} {int(ok)} {lo} {hi} {want} {bound[0]} {bound[1]}")
     dist.barrier()
     dist.destroy_process_group()
 
@@ -156,8 +159,9 @@ def test_gpu_world2_ranks_stitch_to_reference_stream(tmp_path, gpu, orc):
     whole = b"".join(orc.frame(v) for v in values)
     stitched = bytearray(len(whole))
     for r in range(world):
-        off, ok, lo, hi = (tmp_path / f"rank{r}.txt").read_text().split()
+        off, ok, lo, hi, want, b0, b1 = (tmp_path / f"rank{r}.txt").read_text().split()
         assert ok == "1", f"rank {r} round trip"
+        assert want == b0 == b1, f"rank {r} asked for device {want}, kdb_lz4_get_device said {b0} then {b1}"
         data = (tmp_path / f"rank{r}.bin").read_bytes()
         stitched[int(off):int(off) + len(data)] = data
     assert bytes(stitched) == whole
@@ -177,7 +181,10 @@ def test_gpu_host_threads_share_the_library(gpu, orc):
 
     def work(t):
         try:
-            K.set_device(t % K.device_count())
+            want = t % K.device_count()
+            K.set_device(want)
+            if K.get_device() != want:
+                errs.append((t, "bound device", K.get_device(), want))
             vals = oracle.g1_values(pool, 100 + 997 * t, 400) + [bytes(range(256)) * (t + 1)]
             for _ in range(3):
                 fr = K.compress_frames(vals)
@@ -190,6 +197,8 @@ def test_gpu_host_threads_share_the_library(gpu, orc):
                     r, blk = K.compress_limited_output(v, K.compress_bound(len(v)))
                     if blk != orc.compress(v):
                         errs.append((t, "scalar"))
+            if K.get_device() != want:
+                errs.append((t, "device after calls", K.get_device(), want))
         except Exception as e:  # noqa: BLE001
             errs.append((t, repr(e)))
 
