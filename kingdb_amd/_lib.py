@@ -9,7 +9,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkdb_lz4.so")
+# KDB_LZ4_LIB: another build of the same library (A/B variants under
+# kingdb_amd/var/, tools/build_variants.sh); the default is the in-tree build
+LIB_PATH = os.environ.get("KDB_LZ4_LIB") or os.path.join(HERE, "libkdb_lz4.so")
 
 OK = 0
 EINVAL = -1

@@ -142,6 +142,17 @@ struct Table12 {
         : "v"(h & ~3u), "v"(ml), "v"(((p & 0xffu) << sl) & ml), "v"(s.hi), "v"(s.mh),
           "v"((((p >> 8) & 15u) << s.sh) & s.mh)
         : "memory");
+#if KDB_ABL_DUP_XCHG
+    // attribution build (tools/gpurun/lds_attr.sh): the same two exchanges
+    // again as reads (mask 0, data 0), so their LDS bank conflicts count twice
+    uint32_t d0, d1;
+    asm volatile(
+        "ds_mskor_rtn_b32 %0, %2, %4, %4 offset:" KDB_STR(KDB_T12_LO) "\n\t"
+        "ds_mskor_rtn_b32 %1, %3, %4, %4 offset:" KDB_STR(KDB_T12_HI) "\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(d0), "=&v"(d1) : "v"(h & ~3u), "v"(s.hi), "v"(0u) : "memory");
+    asm volatile("" ::"v"(d0), "v"(d1));
+#endif
     return (__builtin_amdgcn_ubfe(oh, s.sh, 4) << 8) | __builtin_amdgcn_ubfe(ol, sl, 8);
   }
   // v: a position < 4096; only lanes whose exchange was on (mh = their nibble mask)
@@ -563,6 +574,14 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // get + put of every valid lane at once, in lane order: refk is the
         // entry as the sequential loop's get at this iteration reads it
         refk = tab.xchg(h, pk, valid, slot);
+#if KDB_ABL_DUP_CAND
+        {  // attribution build: the candidate word read twice (opaque address, so both loads stay)
+          uint32_t r2 = refk;
+          asm volatile("" : "+v"(r2));
+          const uint32_t x = RD32(r2);
+          asm volatile("" ::"v"(x));
+        }
+#endif
         // the lanes whose reference matches (lz4.cc:527, 610-616), as a
         // compare straight into a lane mask (a ballot of a bool would be
         // materialised in a VGPR and compared again); byU32 adds the
