@@ -26,6 +26,7 @@
 
 #include "algorithm/compressor.h"
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -237,6 +238,16 @@ class Pipeline {
 
   void complete(std::vector<Order>& orders);
 
+  // bytes the write buffer accounts for a deferred chunk of `raw` bytes: what
+  // its frame is expected to take, at the compressed/raw ratio of the last
+  // batch (the reference accounts the compressed chunk, write_buffer.cc:170,
+  // which sets its flush cadence and its rate limiter's input)
+  uint64_t accounted(uint64_t raw) const {
+    const uint64_t r = ratio_q16_.load(std::memory_order_relaxed);
+    const uint64_t a = (raw * r) >> 16;
+    return a ? a : 1;
+  }
+
  private:
   void run();
   void drop_consumed();
@@ -269,6 +280,7 @@ class Pipeline {
   Inject inject_;
   uint64_t attempts_ = 0;
   Stats stats_;
+  std::atomic<uint64_t> ratio_q16_{1u << 16};   // accounted / raw bytes of the last batch, x 2^16
 };
 
 void Pipeline::run() {
@@ -537,6 +549,12 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   }
   // each thread's state after its last run of the batch
   for (uint32_t r = 0; r < nruns; r++) state_[run_tid[r]] = cout[r];
+  {  // what the batch's chunks take in the buffer once final, per raw byte
+    uint64_t acc = 0;
+    for (uint32_t q = 0; q < m; q++)
+      acc += parts[q].status == 0 && parts[q].mode != KDB_FLUSH_RAW ? parts[q].size : batch[perm[q]].chunk.size();
+    if (raw_bytes) ratio_q16_.store(std::min<uint64_t>((acc << 16) / raw_bytes, 1u << 17), std::memory_order_relaxed);
+  }
   stats_.batches++;
   stats_.parts += m;
   stats_.raw_bytes += raw_bytes;
@@ -637,6 +655,11 @@ void Pipeline::drop_consumed() {
 }
 
 // ---- registry: one pipeline per write buffer
+// LZ4FlushDefer -> WriteBuffer::WritePart on the same client thread: the
+// bytes to account for the chunk it just queued (LZ4FlushAccount)
+thread_local bool t_account_set = false;
+thread_local uint64_t t_account_raw = 0, t_account = 0;
+
 std::mutex g_mu;
 std::unordered_map<const void*, std::shared_ptr<Pipeline>> g_pipes;
 std::unordered_set<const void*> g_closed;
@@ -667,10 +690,23 @@ Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArra
     t_wb = wb;
     t_pipe = p;
   }
-  return p->defer(key, chunk, offset_chunk, size_value, ticket);
+  const Status s = p->defer(key, chunk, offset_chunk, size_value, ticket);
+  if (s.IsOK()) {
+    t_account_raw = chunk.size();
+    t_account = p->accounted(chunk.size());
+    t_account_set = true;
+  }
+  return s;
+}
+
+uint64_t LZ4FlushAccount(uint64_t chunk_size) {
+  const bool mine = t_account_set && t_account_raw == chunk_size;
+  t_account_set = false;
+  return mine ? t_account : chunk_size;
 }
 
 void LZ4FlushCancel(const void* wb, uint32_t ticket) {
+  t_account_set = false;
   std::shared_ptr<Pipeline> p = pipeline_of(wb, false);
   if (p) p->cancel(ticket);
 }

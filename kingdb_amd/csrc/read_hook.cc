@@ -11,12 +11,18 @@
 // ends in frames.  kdb_get_values_batch's verify mode 2 is exactly that check.
 #include "interface/lz4_read.h"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 #include "../../include/kdb_lz4.h"
 #include "../../include/kdb_put.h"
 #include "algorithm/compressor.h"
+#include "storage/format.h"
+#include "algorithm/crc32c.h"
 
 namespace kdb {
 
@@ -83,15 +89,42 @@ struct ReadStaging {
 
 Status decode_failed() { return Status::IOError("LZ4_decompress_safe_partial() failed"); }
 
+// KDB_LZ4_READ_STATS=1: per-process totals printed at exit ("lz4_read_stats ...")
+struct ReadStats {
+  bool on = getenv("KDB_LZ4_READ_STATS") != nullptr;
+  std::mutex mu;
+  double peek_ms = 0, stage_ms = 0, gpu_ms = 0, arena_ms = 0, join_ms = 0, sync_ms = 0;
+  uint64_t batches = 0, values = 0, stored = 0, gets = 0, sync_batches = 0;
+  ~ReadStats() {
+    if (on)
+      fprintf(stderr,
+              "lz4_read_stats batches %llu values %llu stored_bytes %llu gets %llu peek_ms %.2f stage_ms %.2f "
+              "gpu_ms %.2f arena_ms %.2f join_ms %.2f sync_batches %llu sync_ms %.2f\n",
+              (unsigned long long)batches, (unsigned long long)values, (unsigned long long)stored,
+              (unsigned long long)gets, peek_ms, stage_ms, gpu_ms, arena_ms, join_ms,
+              (unsigned long long)sync_batches, sync_ms);
+  }
+  void add(double& x, double ms) {
+    std::lock_guard<std::mutex> l(mu);
+    x += ms;
+  }
+};
+ReadStats g_read_stats;
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
 // One batch through kdb_get_values_batch; status codes (get.hip): 0, -1 a frame
 // failed, -2 checksum, KDB_LZ4_VALUE_UNSUPPORTED.  out_len = bytes defined.
-int gpu_decode(std::vector<ByteArray>& values, bool verify, ByteArray* arena, std::vector<uint64_t>* out_at,
-               std::vector<uint64_t>* out_len, std::vector<int32_t>* status) {
-  const uint32_t n = (uint32_t)values.size();
+// The decoded values land back to back (64-byte aligned) in one arena.
+int gpu_decode(ReadStaging& stg, const LZ4Stored* values, uint32_t n, bool verify, ByteArray* arena,
+               std::vector<uint64_t>* out_at, std::vector<uint64_t>* out_len, std::vector<int32_t>* status) {
+  const bool stats = g_read_stats.on;
+  Clock::time_point t0 = stats ? Clock::now() : Clock::time_point();
   uint64_t sbytes = 0, obytes = 0, frame_cap = 0, max_in = 0, max_out = 0;
-  for (ByteArray& v : values) {
-    const CompressorLZ4::StoredView w = CompressorLZ4::View(v);
-    const uint64_t svc = w.size_compressed, sz = w.size;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint64_t svc = values[i].size_compressed, sz = values[i].size;
     if (svc > 0xFFFFFFFFull || sz > 0xFFFFFFFFull) return KDB_LZ4_EUNSUPPORTED;
     sbytes += a64(svc);
     obytes += a64(sz);
@@ -106,27 +139,30 @@ int gpu_decode(std::vector<ByteArray>& values, bool verify, ByteArray* arena, st
   const uint64_t o_out = a64(in_bytes), scratch = kdb_get_scratch_bytes(n, frame_cap),
                  o_scr = a64(o_out + obytes + 64), dev_bytes = o_scr + scratch;
   const uint64_t h_out = a64(in_bytes), host_bytes = h_out + obytes + 64;
-  thread_local ReadStaging stg;
   if (!stg.reserve(host_bytes, dev_bytes)) return KDB_LZ4_EHIP;
   char* hb = static_cast<char*>(stg.host);
   char* db = static_cast<char*>(stg.dev);
   auto H64 = [&](uint64_t o) { return reinterpret_cast<uint64_t*>(hb + o); };
   auto H32 = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(hb + o); };
   uint64_t so = 0, oo = 0;
+  uint64_t *soff = H64(o_soff), *avail = H64(o_avail), *svcs = H64(o_svc), *sizes = H64(o_size), *ooff = H64(o_ooff);
+  uint32_t *ck = H32(o_ck), *ci = H32(o_ci);
   for (uint32_t i = 0; i < n; i++) {
-    ByteArray& v = values[i];
-    const CompressorLZ4::StoredView w = CompressorLZ4::View(v);
-    const uint64_t svc = w.size_compressed;
-    H64(o_soff)[i] = so;
-    H64(o_avail)[i] = svc;
-    H64(o_svc)[i] = svc;
-    H64(o_size)[i] = w.size;
-    H64(o_ooff)[i] = oo;
-    H32(o_ck)[i] = w.checksum;
-    H32(o_ci)[i] = w.checksum_initial;
-    memcpy(hb + o_stored + so, v.data(), svc);
-    so += a64(svc);
+    const LZ4Stored& w = values[i];
+    soff[i] = so;
+    avail[i] = w.size_compressed;
+    svcs[i] = w.size_compressed;
+    sizes[i] = w.size;
+    ooff[i] = oo;
+    ck[i] = w.checksum;
+    ci[i] = w.checksum_initial;
+    memcpy(hb + o_stored + so, w.data, w.size_compressed);
+    so += a64(w.size_compressed);
     oo += a64(w.size);
+  }
+  if (stats) {
+    g_read_stats.add(g_read_stats.stage_ms, ms_since(t0));
+    t0 = Clock::now();
   }
   void* st = stg.stream;
   auto D8 = [&](uint64_t o) { return reinterpret_cast<uint8_t*>(db + o); };
@@ -145,18 +181,36 @@ int gpu_decode(std::vector<ByteArray>& values, bool verify, ByteArray* arena, st
     stg.drop();
     return rc;
   }
+  if (stats) {
+    g_read_stats.add(g_read_stats.gpu_ms, ms_since(t0));
+    t0 = Clock::now();
+  }
   char* a = new char[obytes + 1];
   memcpy(a, hb + h_out, obytes);
   *arena = NewShallowCopyByteArray(a, obytes + 1);
   out_at->resize(n);
   out_len->resize(n);
   status->resize(n);
+  const uint64_t* olen = H64(o_olen);
+  const int32_t* stw = reinterpret_cast<const int32_t*>(hb + o_st);
   for (uint32_t i = 0; i < n; i++) {
-    (*out_at)[i] = H64(o_ooff)[i];
-    (*out_len)[i] = H64(o_olen)[i];
-    (*status)[i] = reinterpret_cast<const int32_t*>(hb + o_st)[i];
+    (*out_at)[i] = ooff[i];
+    (*out_len)[i] = olen[i];
+    (*status)[i] = stw[i];
+  }
+  if (stats) {
+    g_read_stats.add(g_read_stats.arena_ms, ms_since(t0));
+    std::lock_guard<std::mutex> l(g_read_stats.mu);
+    g_read_stats.batches++;
+    g_read_stats.values += n;
+    g_read_stats.stored += sbytes;
   }
   return KDB_LZ4_OK;
+}
+
+LZ4Stored stored_of(ByteArray& v) {
+  const CompressorLZ4::StoredView w = CompressorLZ4::View(v);
+  return LZ4Stored{v.data(), w.size_compressed, w.size, w.checksum, w.checksum_initial};
 }
 
 }  // namespace
@@ -168,7 +222,11 @@ bool LZ4DecodeValues(std::vector<ByteArray>& values, bool verify, std::vector<By
   ByteArray arena;
   std::vector<uint64_t> at, len;
   std::vector<int32_t> status;
-  if (gpu_decode(values, verify, &arena, &at, &len, &status) != KDB_LZ4_OK) {
+  std::vector<LZ4Stored> recs;
+  recs.reserve(values.size());
+  for (ByteArray& v : values) recs.push_back(stored_of(v));
+  thread_local ReadStaging stg;
+  if (gpu_decode(stg, recs.data(), (uint32_t)recs.size(), verify, &arena, &at, &len, &status) != KDB_LZ4_OK) {
     for (Status& s : *st) s = Status::IOError("GPU decode batch failed");
     return false;
   }
@@ -181,39 +239,224 @@ bool LZ4DecodeValues(std::vector<ByteArray>& values, bool verify, std::vector<By
 }
 
 // ------------------------------------------------------------- LZ4ReadAhead
+namespace {
+
+// Pinned/device staging for the read-ahead's helper threads: a few sets, kept
+// for the process (a helper thread lives for one batch).
+struct StagingPool {
+  std::mutex mu;
+  std::vector<ReadStaging*> free;
+  ReadStaging* take() {
+    std::lock_guard<std::mutex> l(mu);
+    if (free.empty()) return new ReadStaging();
+    ReadStaging* s = free.back();
+    free.pop_back();
+    return s;
+  }
+  void give(ReadStaging* s) {
+    std::lock_guard<std::mutex> l(mu);
+    if (free.size() < 4) {
+      free.push_back(s);
+      return;
+    }
+    delete s;
+  }
+};
+StagingPool g_read_pool;
+
+// The entries a plan names, headers decoded as Next() decodes them
+// (EntryHeader::DecodeFrom, storage/format.h); *resume: where the next plan
+// starts (0: the plan's entries are exhausted).  The values GetValue would
+// refuse (over the multipart threshold) are left out.
+void decode_plan(const LZ4PeekPlan& plan, uint64_t max_size, size_t max_values, std::vector<LZ4Stored>* recs,
+                 uint64_t* resume) {
+  *resume = 0;
+  if (!plan.base) return;
+  const bool verify = plan.read_options.verify_checksums;
+  uint64_t bytes = 0;
+  auto take = [&](uint64_t off, EntryHeader& h, uint32_t hs) {
+    if (h.size_value_compressed == 0 || h.size_value > max_size) return;
+    const uint32_t ci = verify ? crc32c::Value(plan.base + off + hs, h.size_key) : 0;
+    recs->push_back(LZ4Stored{plan.base + off + hs + h.size_key, h.size_value_compressed, h.size_value,
+                              h.checksum_content, ci});
+    bytes += h.size_value_compressed;
+  };
+  if (!plan.sequential) {
+    for (size_t k = 0; k < plan.offsets.size(); k++) {
+      if (recs->size() >= max_values || bytes >= LZ4ReadAhead::kMaxBytes) {
+        *resume = plan.offsets[k];
+        return;
+      }
+      const uint64_t off = plan.offsets[k];
+      EntryHeader h;
+      uint32_t hs;
+      if (off >= plan.filesize ||
+          !EntryHeader::DecodeFrom(plan.db_options, plan.read_options, plan.base + off, plan.filesize - off, &h, &hs)
+               .IsOK() ||
+          !h.AreSizesValid(off, plan.filesize) || !h.IsEntryFull() || h.IsTypeDelete())
+        continue;
+      take(off, h, hs);
+    }
+    // every listed entry taken: the next plan starts after the last one (the
+    // iterator's locations may go on past what this plan listed)
+    if (!plan.offsets.empty()) *resume = (uint64_t)plan.offsets.back() + 1;
+    return;
+  }
+  uint64_t off = plan.from;
+  while (off < plan.to) {
+    if (recs->size() >= max_values || bytes >= LZ4ReadAhead::kMaxBytes) {
+      *resume = off;
+      return;
+    }
+    EntryHeader h;
+    uint32_t hs;
+    if (!EntryHeader::DecodeFrom(plan.db_options, plan.read_options, plan.base + off, plan.filesize - off, &h, &hs)
+             .IsOK() ||
+        !h.AreSizesValid(off, plan.filesize))
+      return;
+    take(off, h, hs);
+    off += hs + h.size_key + h.size_value_offset();
+  }
+}
+
+}  // namespace
+
+struct LZ4ReadAhead::Batch {
+  struct Decoded {
+    const char* stored;          // the value's stored bytes (its identity while the batch lives)
+    uint64_t at, size;           // its decoded bytes in arena
+    int32_t status;              // kdb_get_values_batch's status word
+  };
+  std::vector<Decoded> d;        // in iteration order
+  ByteArray arena;               // the decoded values, back to back
+  bool ok = false;
+  uint64_t resume = 0;           // where the plan after this batch's starts (0: none)
+  std::thread th;                // the helper building it (a batch ahead)
+  // `first` (the value GetValue asked for, or none) and the plan's entries,
+  // through one GPU batch; on a helper thread, device is the asking thread's
+  void build(const LZ4PeekPlan& plan, const LZ4Stored* first, uint64_t max_size, int device) {
+    const bool stats = g_read_stats.on;
+    const Clock::time_point t0 = stats ? Clock::now() : Clock::time_point();
+    if (device >= 0 && kdb_lz4_set_device(device) != KDB_LZ4_OK) return;
+    std::vector<LZ4Stored> recs;
+    recs.reserve(first ? 1024 : plan.offsets.size() + 1);
+    if (first) recs.push_back(*first);
+    decode_plan(plan, max_size, max_values() - recs.size(), &recs, &resume);
+    if (stats) g_read_stats.add(g_read_stats.peek_ms, ms_since(t0));
+    if (recs.empty()) return;
+    std::vector<uint64_t> at, len;
+    std::vector<int32_t> st;
+    ReadStaging* stg = g_read_pool.take();
+    const int rc = gpu_decode(*stg, recs.data(), (uint32_t)recs.size(), plan.read_options.verify_checksums, &arena,
+                              &at, &len, &st);
+    if (rc != KDB_LZ4_OK) {
+      delete stg;                // dropped: a failed batch's buffers are not reused
+      return;
+    }
+    g_read_pool.give(stg);
+    d.reserve(recs.size());
+    for (size_t j = 0; j < recs.size(); j++) d.push_back(Decoded{recs[j].data, at[j], recs[j].size, st[j]});
+    ok = true;
+  }
+};
+
+size_t LZ4ReadAhead::max_values() {
+  static const size_t n = [] {
+    const char* e = getenv("KDB_LZ4_READ_BATCH");
+    const long v = e ? atol(e) : 0;
+    return v >= 16 && (size_t)v < kMaxValues ? (size_t)v : kMaxValues;
+  }();
+  return n;
+}
+
+LZ4ReadAhead::LZ4ReadAhead() : cur_(new Batch()), next_(nullptr) {}
+
+LZ4ReadAhead::~LZ4ReadAhead() {
+  if (next_) {
+    if (next_->th.joinable()) next_->th.join();
+    delete next_;
+  }
+  delete cur_;
+}
+
+// The batch after cur_, on its own thread (the plan is taken here, on the
+// iterator's thread: it reads the iterator's locations).
+void LZ4ReadAhead::start_next(const Peek& peek, uint64_t max_size) {
+  if (next_ || !cur_->ok || cur_->resume == 0) return;
+  LZ4PeekPlan plan;
+  peek(&plan, cur_->resume);
+  if (!plan.base) return;
+  int device = 0;
+  if (kdb_lz4_get_device(&device) != KDB_LZ4_OK) return;
+  next_ = new Batch();
+  Batch* b = next_;
+  b->th = std::thread([b, max_size, device](LZ4PeekPlan pl) { b->build(pl, nullptr, max_size, device); },
+                      std::move(plan));
+}
+
+// Waits for the batch ahead and makes it current.
+bool LZ4ReadAhead::take_next() {
+  if (!next_) return false;
+  const Clock::time_point t0 = g_read_stats.on ? Clock::now() : Clock::time_point();
+  if (next_->th.joinable()) next_->th.join();
+  if (g_read_stats.on) g_read_stats.add(g_read_stats.join_ms, ms_since(t0));
+  delete cur_;
+  cur_ = next_;
+  next_ = nullptr;
+  cursor_ = 0;
+  return cur_->ok;
+}
+
 ByteArray LZ4ReadAhead::Get(const ReadOptions& read_options, ByteArray& value, uint64_t max_size, Status* status,
                             const Peek& peek) {
   // the iterator asks in order: the expected value, or one a little further
   // on (entries Next() skipped); anything else starts a new batch
   const char* key = value.data();
-  size_t i = cursor_;
-  while (i < batch_.size() && i < cursor_ + 64 && batch_[i].stored != key) i++;
-  if (i >= batch_.size() || batch_[i].stored != key || batch_[i].out.size() != value.size()) {
-    std::vector<ByteArray> batch;
-    batch.push_back(value);
-    std::vector<ByteArray> ahead;
-    peek(&ahead);
-    uint64_t bytes = CompressorLZ4::View(value).size_compressed;
-    for (ByteArray& v : ahead) {
-      if (batch.size() >= kMaxValues || bytes >= kMaxBytes) break;
-      const uint64_t svc = CompressorLZ4::View(v).size_compressed;
-      if (svc == 0 || v.size() > max_size) continue;
-      batch.push_back(v);
-      bytes += svc;
-    }
-    std::vector<ByteArray> out;
-    std::vector<Status> st;
-    LZ4DecodeValues(batch, read_options.verify_checksums, &out, &st);
-    batch_.clear();
-    batch_.reserve(batch.size());
-    for (size_t j = 0; j < batch.size(); j++) batch_.push_back(Decoded{batch[j].data(), out[j], st[j]});
-    i = 0;
+  auto find = [&](size_t from) -> size_t {
+    const std::vector<Batch::Decoded>& d = cur_->d;
+    for (size_t i = from; i < d.size() && i < from + 64; i++)
+      if (d[i].stored == key) return d[i].size == value.size() ? i : d.size();
+    return d.size();
+  };
+  size_t i = find(cursor_);
+  bool fresh = false;
+  if (i >= cur_->d.size() && next_) {
+    take_next();
+    i = find(0);
+    fresh = true;
   }
+  if (i >= cur_->d.size()) {
+    // a batch from the iterator's position, this value first, on this thread
+    const Clock::time_point t0 = g_read_stats.on ? Clock::now() : Clock::time_point();
+    if (next_) take_next();
+    delete cur_;
+    cur_ = new Batch();
+    cursor_ = 0;
+    LZ4PeekPlan plan;
+    peek(&plan, 0);
+    const LZ4Stored first = stored_of(value);
+    cur_->build(plan, &first, max_size, -1);
+    if (!cur_->ok) {
+      *status = Status::IOError("GPU decode batch failed");
+      return ByteArray();
+    }
+    i = 0;
+    fresh = true;
+    if (g_read_stats.on) {
+      g_read_stats.add(g_read_stats.sync_ms, ms_since(t0));
+      std::lock_guard<std::mutex> l(g_read_stats.mu);
+      g_read_stats.sync_batches++;
+    }
+  }
+  if (fresh) start_next(peek, max_size);
   cursor_ = i + 1;
-  *status = batch_[i].st;
-  ByteArray r = batch_[i].out;
-  batch_[i].out = ByteArray();
-  return r;
+  const Batch::Decoded& d = cur_->d[i];
+  *status = d.status == 0 ? Status::OK() : d.status == -2 ? Status::IOError("Invalid checksum.") : decode_failed();
+  if (g_read_stats.on) {
+    std::lock_guard<std::mutex> l(g_read_stats.mu);
+    g_read_stats.gets++;
+  }
+  return CompressorLZ4::Slice(cur_->arena, d.at, d.size);
 }
 
 // ------------------------------------------------------- LZ4MultipartDecode
@@ -248,11 +491,12 @@ void LZ4MultipartDecode::Prepare(const ReadOptions& read_options, ByteArray& val
     off += c > 0 ? (uint64_t)c : 8ull + sz;
   }
   if (!tail && off != svc) return;
-  std::vector<ByteArray> one{value};
+  const LZ4Stored one = stored_of(value);
   ByteArray arena;
   std::vector<uint64_t> at, len;
   std::vector<int32_t> status;
-  if (gpu_decode(one, read_options.verify_checksums, &arena, &at, &len, &status) != KDB_LZ4_OK) return;
+  thread_local ReadStaging stg;
+  if (gpu_decode(stg, &one, 1, read_options.verify_checksums, &arena, &at, &len, &status) != KDB_LZ4_OK) return;
   out_ = CompressorLZ4::Slice(arena, at[0], value.size());
   active_ = true;
   fail_at_end_ = status[0] == -1 || status[0] == KDB_LZ4_VALUE_UNSUPPORTED;

@@ -54,6 +54,11 @@ Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArra
                      uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket);
 // The order of `ticket` never reached the buffer (WriteBuffer::PutPart failed).
 void LZ4FlushCancel(const void* wb, uint32_t ticket);
+// WriteBuffer::WritePart, same client thread, right after LZ4FlushDefer: the
+// bytes to account for the raw chunk it queued -- its expected frame size,
+// as the reference accounts the compressed chunk -- or chunk_size for any
+// other order.
+uint64_t LZ4FlushAccount(uint64_t chunk_size);
 
 // Flush thread, buffer readers held off.  Completes every deferred order of
 // `orders` in place; an order whose PutPartValidSize call fails (IOError

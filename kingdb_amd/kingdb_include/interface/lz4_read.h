@@ -38,24 +38,60 @@ namespace kdb {
 bool LZ4DecodeValues(std::vector<ByteArray>& values, bool verify, std::vector<ByteArray>* out,
                      std::vector<Status>* st);
 
+// A stored value as the read-ahead needs it: no ByteArray per value (each one
+// is a shared resource to reference-count), the bytes stay in the file mapping.
+struct LZ4Stored {
+  const char* data;            // the stored bytes (size_compressed of them)
+  uint64_t size_compressed, size;
+  uint32_t checksum, checksum_initial;
+};
+
+// What an iterator's peek hands the read-ahead: which entries of the current
+// HSTable come next, not yet decoded -- the entry headers are read by the
+// read-ahead (on its helper thread for the batches ahead), from the mapping
+// `keep` holds alive.  RegularIterator lists entry offsets (its sorted
+// locations, storage_engine.h); SequentialIterator gives a byte range walked
+// entry by entry, as its Next() walks it.
+struct LZ4PeekPlan {
+  ByteArray keep;                  // a view of the file's mapping (empty: nothing to peek)
+  const char* base = nullptr;      // the mapping as the iterator's values address it
+  uint64_t filesize = 0;
+  bool sequential = false;
+  std::vector<uint32_t> offsets;   // regular: the entries' offsets, ascending
+  uint64_t from = 0, to = 0;       // sequential: entries starting in [from, to)
+  DatabaseOptions db_options;
+  ReadOptions read_options;
+};
+
 class LZ4ReadAhead {
  public:
   static constexpr size_t kMaxValues = 65536;           // values per batch
+  // kMaxValues, or KDB_LZ4_READ_BATCH (16 .. kMaxValues) where set: tests use
+  // small batches to run the helper threads on small databases
+  static size_t max_values();
   static constexpr uint64_t kMaxBytes = 64ull << 20;    // stored bytes per batch
-  using Peek = std::function<void(std::vector<ByteArray>*)>;
+  // fills a plan for up to kMaxValues entries after `resume` (0: after the
+  // iterator's current entry; else the offset the previous plan ended at)
+  using Peek = std::function<void(LZ4PeekPlan*, uint64_t resume)>;
+  LZ4ReadAhead();
+  ~LZ4ReadAhead();
+  LZ4ReadAhead(const LZ4ReadAhead&) = delete;
+  LZ4ReadAhead& operator=(const LZ4ReadAhead&) = delete;
   // GetValue of a compressed `value`; the peeked values above max_size (the
-  // multipart threshold, which GetValue refuses) are left out of the batch
+  // multipart threshold, which GetValue refuses) are left out of the batch.
+  // When a batch is installed, the next one is decoded on a helper thread
+  // while this one is consumed.
   ByteArray Get(const ReadOptions& read_options, ByteArray& value, uint64_t max_size, Status* status,
                 const Peek& peek);
 
+  struct Batch;                  // read_hook.cc
+
  private:
-  struct Decoded {
-    const char* stored;   // the value's stored bytes (its identity while the batch lives)
-    ByteArray out;
-    Status st;
-  };
-  std::vector<Decoded> batch_;   // in iteration order
-  size_t cursor_ = 0;            // the next value GetValue is expected to ask for
+  Batch* cur_;                   // the batch GetValue is served from
+  Batch* next_;                  // the one being decoded ahead (its own thread), or none
+  size_t cursor_ = 0;            // the next value of cur_ GetValue is expected to ask for
+  void start_next(const Peek& peek, uint64_t max_size);
+  bool take_next();
 };
 
 class LZ4MultipartDecode {

@@ -46,65 +46,53 @@ GETVALUE_OLD = """    // TODO-36: Uncompression should not have to go through a 
 """
 GETVALUE_NEW = """    // this value and the next entries' values, decoded in one GPU batch (LZ4ReadAhead)
     return lz4_read_ahead_.Get(read_options_, value_, se_readonly_->db_options_.internal__size_multipart_required,
-                               &status_, [this](std::vector<ByteArray>* ahead) { LZ4PeekAhead(ahead); });
+                               &status_, [this](LZ4PeekPlan* plan, uint64_t resume) { LZ4PeekAhead(plan, resume); });
 """
 REGULAR_PEEK = """  LZ4ReadAhead lz4_read_ahead_;
   // the entries Next() will visit in the current HSTable (some may be skipped
-  // there as overwritten: decoding them is only wasted work); after the first
-  // (StorageEngine::GetEntry, storage_engine.h:459-521) the headers are decoded
-  // straight from the same pooled mapping of the file
-  void LZ4PeekAhead(std::vector<ByteArray>* ahead) {
-    ByteArray file;
-    for (uint32_t i = index_location_; i < locations_current_.size() && ahead->size() < LZ4ReadAhead::kMaxValues; i++) {
-      const uint64_t location = locations_current_[i];
-      if (!file.resource_) {
-        ByteArray key, value;
-        if (!se_readonly_->GetEntry(read_options_, location, &key, &value).IsOK()) continue;
-        ahead->push_back(value);
-        file = value;
-        continue;
-      }
-      const uint32_t off = (uint32_t)(location & 0xFFFFFFFF);
-      const uint64_t filesize = file.resource_->size();
-      const char* base = file.resource_->data();
-      struct EntryHeader h;
-      uint32_t hs;
-      if (off >= filesize ||
-          !EntryHeader::DecodeFrom(se_readonly_->db_options_, read_options_, base + off, filesize - off, &h, &hs).IsOK() ||
-          !h.AreSizesValid(off, filesize) || !h.IsEntryFull() || h.IsTypeDelete())
-        continue;
-      ByteArray value = file;
-      if (read_options_.verify_checksums) value.set_checksum_initial(crc32c::Value(base + off + hs, h.size_key));
-      value.set_offset(off + hs + h.size_key);
-      value.set_size(h.size_value);
-      value.set_size_compressed(h.size_value_compressed);
-      value.set_checksum(h.checksum_content);
-      ahead->push_back(value);
+  // there as overwritten: decoding them is only wasted work), as offsets into
+  // the pooled mapping StorageEngine::GetEntry hands out (storage_engine.h:
+  // 459-521); locations_current_ is sorted, so `resume` (an offset) is found
+  // by binary search
+  void LZ4PeekAhead(LZ4PeekPlan* plan, uint64_t resume) {
+    size_t i = index_location_;
+    if (resume) {
+      const uint64_t file_bits = index_location_ < locations_current_.size()
+                                     ? (locations_current_[index_location_] & 0xFFFFFFFF00000000ULL)
+                                     : (locations_current_.empty() ? 0 : locations_current_.back() & 0xFFFFFFFF00000000ULL);
+      i = std::lower_bound(locations_current_.begin(), locations_current_.end(), file_bits | resume) -
+          locations_current_.begin();
+    }
+    if (i >= locations_current_.size()) return;
+    ByteArray key, value;
+    if (!se_readonly_->GetEntry(read_options_, locations_current_[i], &key, &value).IsOK() || !value.resource_) return;
+    plan->keep = value;
+    plan->base = value.resource_->data();
+    plan->filesize = value.resource_->size();
+    plan->db_options = se_readonly_->db_options_;
+    plan->read_options = read_options_;
+    const uint64_t file_bits = locations_current_[i] & 0xFFFFFFFF00000000ULL;
+    for (; i < locations_current_.size() && plan->offsets.size() < LZ4ReadAhead::max_values(); i++) {
+      if ((locations_current_[i] & 0xFFFFFFFF00000000ULL) != file_bits) break;
+      plan->offsets.push_back((uint32_t)(locations_current_[i] & 0xFFFFFFFF));
     }
   }
 """
 SEQUENTIAL_PEEK = """  LZ4ReadAhead lz4_read_ahead_;
-  // the entries Next() will visit in the current HSTable, decoded as Next() decodes them
-  void LZ4PeekAhead(std::vector<ByteArray>* ahead) {
-    if (!has_file_ || !mmap_.is_valid()) return;
-    uint64_t off = offset_;
-    while (off < offset_end_ && ahead->size() < LZ4ReadAhead::kMaxValues) {
-      struct EntryHeader h;
-      uint32_t hs;
-      Status s = EntryHeader::DecodeFrom(se_readonly_->db_options_, read_options_, mmap_.datafile() + off,
-                                         mmap_.filesize() - off, &h, &hs);
-      if (!s.IsOK() || !h.AreSizesValid(off, mmap_.filesize())) break;
-      ByteArray value = ByteArray::NewPooledByteArray(se_readonly_->file_manager_, fileid_current_,
-                                                      filepath_current_, mmap_.filesize_);
-      if (read_options_.verify_checksums)
-        value.set_checksum_initial(crc32c::Value(value.data() + off + hs, h.size_key));
-      value.set_offset(off + hs + h.size_key);
-      value.set_size(h.size_value);
-      value.set_size_compressed(h.size_value_compressed);
-      value.set_checksum(h.checksum_content);
-      ahead->push_back(value);
-      off += hs + h.size_key + h.size_value_offset();
-    }
+  // the entries Next() will visit in the current HSTable: the bytes from
+  // `resume` (or Next()'s offset_) to offset_end_, walked as Next() walks them,
+  // addressed in the same pooled mapping as value_'s (Next()'s values are
+  // views of it, so the read-ahead recognises them)
+  void LZ4PeekAhead(LZ4PeekPlan* plan, uint64_t resume) {
+    if (!has_file_ || !mmap_.is_valid() || !value_.resource_) return;
+    plan->keep = value_;
+    plan->base = value_.resource_->data();
+    plan->filesize = mmap_.filesize();
+    plan->sequential = true;
+    plan->from = resume ? resume : offset_;
+    plan->to = offset_end_;
+    plan->db_options = se_readonly_->db_options_;
+    plan->read_options = read_options_;
   }
 """
 READ_INCLUDE = '#include "interface/lz4_read.h"\n'
@@ -126,6 +114,8 @@ EDITS = {
          "  bool do_compression = true;\n  uint64_t size_value_compressed = 0;\n"),
     ],
     "cache/write_buffer.cc": [
+        ("  bytes_arriving += chunk.size();\n",
+         "  bytes_arriving += LZ4FlushAccount(chunk.size());   // a deferred chunk: its expected frame size\n"),
         ('#include "cache/write_buffer.h"\n', '#include "cache/write_buffer.h"\n' + INCLUDE),
         ("void WriteBuffer::ProcessingLoop() {\n",
          "void WriteBuffer::ProcessingLoop() {\n"

@@ -256,9 +256,9 @@ def test_hook_client_embedded_iteration_vs_reference(tmp_path, gpu):
         wd = tmp_path / b
         wd.mkdir()
         r = subprocess.run([_bin(d, "client_emb")], cwd=wd, capture_output=True, text=True, timeout=600,
-                           env=dict(os.environ, KDB_LZ4_FLUSH_STATS="1"))
+                           env=dict(os.environ, KDB_LZ4_FLUSH_STATS="1", KDB_LZ4_READ_STATS="1"))
         for ln in r.stderr.splitlines():
-            if ln.startswith("lz4_flush_stats"):
+            if ln.startswith(("lz4_flush_stats", "lz4_read_stats")):
                 print(b, ln)
         assert r.returncode == 0, r.stderr[-2000:]
         assert "count items: 1000000" in r.stdout
@@ -274,6 +274,6 @@ def test_hook_concurrent_writers_and_readers(tmp_path, gpu):
     PutPartValidSize state), then 8 readers (Get, MultipartReader) and an
     iteration get every value back byte for byte."""
     r = subprocess.run([_bin(HOOK, "hook_mt"), str(tmp_path / "db"), "8", "150"], capture_output=True, text=True,
-                       timeout=600)
+                       timeout=600, env=dict(os.environ, KDB_LZ4_READ_BATCH="64"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.startswith("ok:"), r.stdout

@@ -92,7 +92,8 @@ def test_kingdb_hook_threads_tsan(tmp_path):
     flush hook, then 4 readers (Get, MultipartReader) and an iteration through
     the read hooks; no race in our code."""
     _make(["-C", ORACLE, "kingdb_san", "SAN=thread"])
-    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=0 history_size=4")
+    # small read-ahead batches, so the iteration runs its helper threads too
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=0 history_size=4", KDB_LZ4_READ_BATCH="32")
     r = subprocess.run([os.path.join(ORACLE, "_ref", "kingdb_tsan", "hook_mt"), str(tmp_path / "db"), "4", "60"],
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -106,7 +107,7 @@ def test_kingdb_hook_asan(tmp_path):
     """The same driver and the golden write streams (kdb_db, then --verify's
     Get / iterator / MultipartReader reads) under AddressSanitizer."""
     _make(["-C", ORACLE, "kingdb_san", "SAN=address"])
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", KDB_LZ4_READ_BATCH="32")
     exe = os.path.join(ORACLE, "_ref", "kingdb_asan")
     r = subprocess.run([os.path.join(exe, "hook_mt"), str(tmp_path / "mt"), "4", "40"], capture_output=True,
                        text=True, timeout=900, env=env)
