@@ -148,6 +148,12 @@ int kdb_lz4_pack_frames(void* stream, const uint8_t* src, const uint64_t* src_of
                         const uint32_t* len, uint32_t n, uint8_t* dst, uint64_t* dst_off,
                         uint64_t* total);
 
+/* *out (device pointer) = the largest of v[0..n) (device array), 0 for n = 0:
+ * e.g. the largest frame of a device-resident batch, for the max_in argument
+ * of kdb_lz4_decompress_frames_batch when the caller holds no host copy of
+ * the frame lengths. */
+int kdb_lz4_max_u32(void* stream, const uint32_t* v, uint32_t n, uint32_t* out);
+
 /* ----------------------------------------------------------- data helpers */
 
 /* Synthetic G1 ("db_bench") data on the device: 100-byte pieces first_piece ..

@@ -318,18 +318,22 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
 // 16-byte chunks, so a value's start does not wait for two HBM round trips
 // (header, then block).  Values whose bytes do not fit kDPrefetch chunks per
 // lane (or the staging area) get chunks = 0 and are staged as before.
-constexpr uint32_t kDPrefetch = 5;
-__device__ __forceinline__ void prefetch_value(uint4& p0, uint4& p1, uint4& p2, uint4& p3, uint4& p4, uint32_t& head, uint32_t& chunks, uint32_t w,
-                                               uint32_t n, const uint8_t* __restrict__ src,
-                                               const uint64_t* __restrict__ src_off,
+// kPF chunks of 16 B per lane: 5 hold any frame of a <= 4 KiB value (8 +
+// compressBound(4096) bytes); 3 hold a frame of up to 3 057 bytes, and free 8
+// VGPRs (launch_one picks 3 when the batch's max_in allows it).
+template <uint32_t kPF>
+__device__ __forceinline__ void prefetch_value(uint4& p0, uint4& p1, uint4& p2, uint4& p3, uint4& p4, uint32_t& head,
+                                               uint32_t& chunks, uint32_t w, uint32_t n,
+                                               const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
                                                const uint32_t* __restrict__ in_len, uint32_t s_in_cap) {
+  static_assert(kPF == 3 || kPF == 5, "3 or 5 chunks per lane");
   chunks = 0;
   if (w >= n) return;
   const uint8_t* gp = src + sload(src_off, w);
   const uint32_t len = sload(in_len, w);
   const uint32_t hd = uni((uint32_t)(reinterpret_cast<uintptr_t>(gp) & 15u));
   const uint32_t ch = (hd + len + 15u) >> 4;
-  if (len == 0 || hd + len + 16u > s_in_cap || ch > 64u * kDPrefetch) return;
+  if (len == 0 || hd + len + 16u > s_in_cap || ch > 64u * kPF) return;
   head = hd;
   chunks = ch;
   const uint4* base = reinterpret_cast<const uint4*>(__builtin_assume_aligned(gp - hd, 16));
@@ -337,11 +341,13 @@ __device__ __forceinline__ void prefetch_value(uint4& p0, uint4& p1, uint4& p2, 
   p0 = base[min(lane, ch - 1u)];
   p1 = base[min(lane + 64u, ch - 1u)];
   p2 = base[min(lane + 128u, ch - 1u)];
-  p3 = base[min(lane + 192u, ch - 1u)];
-  p4 = base[min(lane + 256u, ch - 1u)];
+  if constexpr (kPF == 5) {
+    p3 = base[min(lane + 192u, ch - 1u)];
+    p4 = base[min(lane + 256u, ch - 1u)];
+  }
 }
 
-template <bool kFrame>
+template <bool kFrame, uint32_t kPF>
 __device__ __forceinline__ void small_decode_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
@@ -363,7 +369,7 @@ __device__ __forceinline__ void small_decode_loop(
 
   WorkQueue wq = WorkQueue::make(work, n, batch, nq);
   uint32_t v = uni(wq.next());
-  prefetch_value(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, v, n, src, src_off, in_len, s_in_cap);
+  prefetch_value<kPF>(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, v, n, src, src_off, in_len, s_in_cap);
 #pragma unroll 1
   while (v < n) {
     const uint32_t vn = uni(wq.next());   // the next value, one ahead
@@ -372,14 +378,15 @@ __device__ __forceinline__ void small_decode_loop(
     const uint32_t st_head = pf_head, st_chunks = pf_chunks;
     {
       uint4* l4 = reinterpret_cast<uint4*>(s_in);
-      static_assert(kDPrefetch == 5, "landing below is written out for 5 chunks per lane");
       if (lane < st_chunks) l4[lane] = pf0;
       if (lane + 64u < st_chunks) l4[lane + 64u] = pf1;
       if (lane + 128u < st_chunks) l4[lane + 128u] = pf2;
-      if (lane + 192u < st_chunks) l4[lane + 192u] = pf3;
-      if (lane + 256u < st_chunks) l4[lane + 256u] = pf4;
+      if constexpr (kPF == 5) {
+        if (lane + 192u < st_chunks) l4[lane + 192u] = pf3;
+        if (lane + 256u < st_chunks) l4[lane + 256u] = pf4;
+      }
     }
-    prefetch_value(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, vn, n, src, src_off, in_len, s_in_cap);
+    prefetch_value<kPF>(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, vn, n, src, src_off, in_len, s_in_cap);
     do {
       const uint8_t* g = src + sload(src_off, v);
       uint8_t* o = dst + sload(dst_off, v);
@@ -450,7 +457,7 @@ __device__ __forceinline__ void small_decode_loop(
   }
 }
 
-template <bool kFrame>
+template <bool kFrame, uint32_t kPF>
 __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
     uint32_t skip_big, uint32_t nq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  small_decode_loop<kFrame>(smem, src, src_off, in_len, n, in_cap, out_cap_max, dst, dst_off, out_cap, target,
+  small_decode_loop<kFrame, kPF>(smem, src, src_off, in_len, n, in_cap, out_cap_max, dst, dst_off, out_cap, target,
                             out_len, ret, work, batch, skip_big, nq);
 }
 
@@ -908,7 +915,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
   ring_decode_loop<kFrame, 4096u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
                                   out_len, ret, work_big, batch_big);
   __syncthreads();
-  small_decode_loop<kFrame>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+  small_decode_loop<kFrame, 5u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
                             out_len, ret, work_small, batch_small, 1u, nq);
 }
 
@@ -925,13 +932,17 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
                              uint32_t* out_len, int32_t* ret, uint32_t skip_big) {
-  auto kern = lz4_decompress_kernel<F>;
+  // the register prefetch's depth: 3 chunks per lane when every frame of the
+  // launch fits them (8 fewer VGPRs: 6 waves per SIMD instead of 5)
+  const bool pf3 = max_in <= 3057u;
+  auto kern = pf3 ? lz4_decompress_kernel<F, 3u> : lz4_decompress_kernel<F, 5u>;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t* work = nullptr;
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = claim_batch(n, grid);
-  launch_note(F ? "lz4_decompress_kernel<true>" : "lz4_decompress_kernel<false>");
+  launch_note(F ? (pf3 ? "lz4_decompress_kernel<true, 3u>" : "lz4_decompress_kernel<true, 5u>")
+                : (pf3 ? "lz4_decompress_kernel<false, 3u>" : "lz4_decompress_kernel<false, 5u>"));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
                      out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out));
   e = hipGetLastError();

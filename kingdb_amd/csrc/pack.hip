@@ -204,9 +204,28 @@ __global__ __launch_bounds__(256) void pack_copy_kernel(const uint8_t* __restric
   }
 }
 
+// *out = max(*out, v[0..n)): grid-stride, a wave-wide max, one atomicMax per wave
+__global__ __launch_bounds__(256) void max_u32_kernel(const uint32_t* __restrict__ v, uint32_t n,
+                                                      uint32_t* __restrict__ out) {
+  uint32_t m = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) m = max(m, v[i]);
+  for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d));
+  if (lane_id() == 0 && m) atomicMax(out, m);
+}
+
 }  // namespace kdb_lz4
 
 using namespace kdb_lz4;
+
+extern "C" int kdb_lz4_max_u32(void* stream, const uint32_t* v, uint32_t n, uint32_t* out) {
+  if ((n && !v) || !out) return KDB_LZ4_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return KDB_LZ4_EHIP;
+  if (n == 0) return KDB_LZ4_OK;
+  const uint32_t blocks = min((n + 255u) / 256u, 1024u);
+  hipLaunchKernelGGL(max_u32_kernel, dim3(blocks), dim3(256), 0, st, v, n, out);
+  return hipGetLastError() == hipSuccess ? KDB_LZ4_OK : KDB_LZ4_EHIP;
+}
 
 extern "C" int kdb_lz4_pack_frames(void* stream, const uint8_t* src, const uint64_t* src_off,
                                    const uint32_t* len, uint32_t n, uint8_t* dst, uint64_t* dst_off,

@@ -353,6 +353,8 @@ class DeviceBatch:
     out: DeviceBuffer
     meta: DeviceBuffer
     slot: int                  # largest frame slot
+    max_in: int = 0            # largest frame decompress() is told to expect (0: the slot)
+    exact_max_in: bool = False # decompress(): find the largest frame on the device first (one 4-byte read back)
 
     @property
     def raw_bytes(self) -> int:
@@ -426,10 +428,28 @@ class DeviceBatch:
             stream.ptr if stream else None, self.src.ptr, self._p(0), self._p(1), self.n, self.size,
             self.frames.ptr, self._p(2), self._p(3), self._p(4)), "compress_frames_batch")
 
+    def largest_frame(self, stream: Stream | None = None) -> int:
+        """The largest frame length of the batch, reduced on the device
+        (kdb_lz4_max_u32) and read back: the max_in a caller with no host copy
+        of the frame lengths passes to the decoder."""
+        if getattr(self, "_maxbuf", None) is None:
+            self._maxbuf = DeviceBuffer(4)
+        st = stream.ptr if stream else None
+        _lib.check(lib().kdb_lz4_max_u32(st, self._p(3), self.n, self._maxbuf.ptr), "max_u32")
+        v = ctypes.c_uint32(0)
+        _lib.check(lib().kdb_lz4_memcpy_d2h(ctypes.addressof(v), self._maxbuf.ptr, 4, st), "d2h")
+        _lib.check(lib().kdb_lz4_stream_sync(st), "sync")
+        return int(v.value)
+
     def decompress(self, stream: Stream | None = None) -> None:
+        if self.exact_max_in:
+            # the decoder's LDS staging is sized by max_in: the frames' true
+            # largest (about 0.56 x 4 KiB for G1) instead of the slot bound
+            # (8 + compressBound) leaves room for more waves per CU
+            self.max_in = max(self.largest_frame(stream), 1)
         _lib.check(lib().kdb_lz4_decompress_frames_batch(
             stream.ptr if stream else None, self.frames.ptr, self._p(2), self._p(3), self.n,
-            self.slot, self.size, self.out.ptr, self._p(5), self._p(6), self._p(7), self._p(8)),
+            self.max_in or self.slot, self.size, self.out.ptr, self._p(5), self._p(6), self._p(7), self._p(8)),
             "decompress_frames_batch")
 
     def frame_lens(self) -> np.ndarray:
@@ -452,5 +472,6 @@ class DeviceBatch:
         return bool(np.array_equal(self.src.download(t), self.out.download(t)))
 
     def free(self) -> None:
-        for b in (self.src, self.frames, self.out, self.meta):
-            b.free()
+        for b in (self.src, self.frames, self.out, self.meta, getattr(self, "_maxbuf", None)):
+            if b is not None:
+                b.free()

@@ -69,4 +69,8 @@ def test_last_kernels_names(gpu):
     K.compress_frames([b"x" * 100000])
     assert "lz4_compress_big_kernel<true, true>" in K.last_kernels()
     K.decompress_frames(K.compress_frames([b"x" * 4096] * 4), [4096] * 4)
-    assert K.last_kernels() == ["lz4_decompress_kernel<true>"]
+    assert K.last_kernels() == ["lz4_decompress_kernel<true, 3u>"]     # every frame <= 3 057 B
+    import numpy as np
+    noise = np.random.default_rng(7).integers(0, 256, 4096, dtype=np.uint8).tobytes()   # a 4 104 B raw frame
+    K.decompress_frames(K.compress_frames([noise, b"x" * 4096]), [4096] * 2)
+    assert K.last_kernels() == ["lz4_decompress_kernel<true, 5u>"]

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--uniform", action="append", default=[],
                     help="SIZE:N extra uniform batch (round-trip gate only, no digest)")
     ap.add_argument("--no-headline", action="store_true")
+    ap.add_argument("--exact-max-in", action="store_true",
+                    help="decompress told the batch's largest frame (not the slot bound)")
     a = ap.parse_args()
     from kingdb_amd import _lib
     _lib.load(os.path.abspath(a.so))
@@ -46,6 +48,7 @@ def main():
     for name, sizes in work:
         b = K.DeviceBatch.g1_long_sizes(sizes)
         st = K.Stream()
+        b.exact_max_in = a.exact_max_in
         b.compress(st)
         b.decompress(st)
         st.sync()
