@@ -74,3 +74,31 @@ def test_last_kernels_names(gpu):
     noise = np.random.default_rng(7).integers(0, 256, 4096, dtype=np.uint8).tobytes()   # a 4 104 B raw frame
     K.decompress_frames(K.compress_frames([noise, b"x" * 4096]), [4096] * 2)
     assert K.last_kernels() == ["lz4_decompress_kernel<true, 5u>"]
+
+
+@pytest.mark.parametrize("n,shift", [(0, 0), (1, 0), (3, 1), (5, 0), (1023, 3), (4096, 0), (65537, 2),
+                                     ((1 << 20) + 3, 1)])
+def test_max_u32_reduction(gpu, n, shift):
+    """kdb_lz4_max_u32 (the decoder's max_in for a device-resident batch):
+    the exact maximum at ragged lengths, 16-byte-aligned or not (shift dwords)."""
+    import ctypes
+
+    import numpy as np
+
+    import kingdb_amd as K
+    from kingdb_amd import _lib
+    from kingdb_amd.lz4 import DeviceBuffer, lib
+    K.set_device(0)
+    rng = np.random.default_rng(n + shift)
+    v = rng.integers(0, 1 << 20, size=n, dtype=np.uint32)
+    if n:
+        v[rng.integers(0, n)] = (1 << 31) + 7          # one large value anywhere (tail included)
+    buf = DeviceBuffer(4 * (n + shift) + 64)
+    if n:
+        buf.upload(v, offset=4 * shift)
+    out = DeviceBuffer(4)
+    _lib.check(lib().kdb_lz4_max_u32(None, buf.ptr + 4 * shift, n, out.ptr), "max_u32")
+    r = ctypes.c_uint32(123)
+    _lib.check(lib().kdb_lz4_memcpy_d2h(ctypes.addressof(r), out.ptr, 4, None), "d2h")
+    _lib.check(lib().kdb_lz4_stream_sync(None), "sync")
+    assert r.value == (int(v.max()) if n else 0)
