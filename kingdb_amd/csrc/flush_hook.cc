@@ -209,15 +209,16 @@ class Pipeline {
     if (stats_.on)
       fprintf(stderr,
               "lz4_flush_stats batches %llu parts %llu raw_bytes %llu stage_ms %.2f gpu_ms %.2f results_ms %.2f "
-              "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f\n",
+              "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f defer_ms %.2f\n",
               (unsigned long long)stats_.batches, (unsigned long long)stats_.parts,
               (unsigned long long)stats_.raw_bytes, stats_.stage_ms, stats_.gpu_ms, stats_.results_ms,
               (unsigned long long)stats_.flushes, (unsigned long long)stats_.orders, (unsigned long long)stats_.waits,
-              stats_.wait_ms, stats_.complete_ms, ms_since(t0));
+              stats_.wait_ms, stats_.complete_ms, ms_since(t0), defer_ns_.load() / 1e6);
   }
 
   Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket) {
     bool kick;
+    const Clock::time_point t0 = stats_.on ? Clock::now() : Clock::time_point();
     {
       std::lock_guard<std::mutex> l(mu_);
       if (failed_) return Status::IOError("LZ4 flush pipeline failed", failure_);
@@ -228,6 +229,8 @@ class Pipeline {
       kick = intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts;
     }
     if (kick) cv_work_.notify_one();
+    if (stats_.on) defer_ns_.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(),
+                                       std::memory_order_relaxed);
     return Status::OK();
   }
 
@@ -280,7 +283,8 @@ class Pipeline {
   Inject inject_;
   uint64_t attempts_ = 0;
   Stats stats_;
-  std::atomic<uint64_t> ratio_q16_{1u << 16};   // accounted / raw bytes of the last batch, x 2^16
+  std::atomic<uint64_t> ratio_q16_{1u << 16};
+  std::atomic<uint64_t> defer_ns_{0};           // client threads' time in defer() (stats only)   // accounted / raw bytes of the last batch, x 2^16
 };
 
 void Pipeline::run() {

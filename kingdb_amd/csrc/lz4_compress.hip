@@ -347,6 +347,16 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // its start is known (at the end of the sequence before), so the read
     // overlaps that sequence's byte store
     typename Src::Word seq0 = src.rd32_issue(clamp4(1u + lane));
+    // In-place values (HBM/L2): a 256-byte register window of the value from
+    // each match's start (one dword per lane, loaded with the count's bytes),
+    // from which the next sequence's input words and -- one sequence later --
+    // its literals come by ds_bpermute instead of two more global round trips
+    // per sequence (the chain is then: exchange, candidate word, count).
+    // A base of 2^31 marks "no window" (positions stay below 2^31).  byU16
+    // values only: for byU32 ones (1 MiB parts) it measured slower (8.47 ->
+    // 9.01 ms per 600 x 1 MiB).
+    constexpr bool kWin = !kFree && !kWide;
+    uint32_t win = 0, wbase = 0x80000000u, pwin = 0, pbase = 0x80000000u;
     // One sequence per call.  The sequence loop runs while anchor < lim_end:
     // mflimit + 1 (lz4.cc:597: a match that ends past mflimit leaves for the
     // last literals), or 0 once a search finds no match (the last literals)
@@ -407,6 +417,12 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // not wait behind it; it lands before the next sequence's exchange
         // all the same (measured: mixed batch compress -2 %; LDS-staged
         // values restore first, below the search: +1.7 % the other way)
+        if constexpr (kWin) {
+          pwin = win;
+          pbase = wbase;
+          wbase = ip;
+          win = src.rd32(min(ip + 4u * lane, last4));
+        }
         if constexpr (!kFree) {
           if (ip - refk < pk - refk) tab.restore(slot, refk);
         }
@@ -518,12 +534,37 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         anchor = ip_end;
         // the next sequence's input words go out before this sequence's
         // bytes, whose literal read shares their round trip
-        seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
         // byte j of the encoding on lane j: token (0), remL (1 if nl1),
         // literals [a, b) with a = 1 + nl1, b = a + lit, the offset LE16 at
         // b, b+1, remM at b+2 (if nm1); lanes past etot are dropped
         const uint32_t da = (lane - 1u) - nl1;        // lane - a: the lane's literal index
-        const uint32_t lb = src.u8(clamp1(seq_anchor + da));
+        uint32_t lb;
+        if constexpr (!kWin) {
+          seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+          lb = src.u8(clamp1(seq_anchor + da));
+        } else {
+          // next input words: bytes ip_end - 2 + lane .. +3, at window offset
+          // ml + 2 + lane (ml before the catch-up); covered while ml <= 187
+          const uint32_t mw = ip_end - wbase;               // 4 + ml
+          if (mw <= 191u) {
+            const uint32_t d = mw - 2u + lane;
+            const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((d >> 2) << 2), (int)win);
+            const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((d >> 2) + 1u) << 2), (int)win);
+            seq0 = typename Src::Word{__builtin_amdgcn_alignbyte(w1, w0, d & 3u)};
+          } else {
+            seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+          }
+          // literals [seq_anchor, seq_anchor + lit): in the previous match's
+          // window when they end inside it
+          const uint32_t lo = seq_anchor - pbase;
+          if (lo + lit <= 256u) {
+            const uint32_t o = lo + da;
+            const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((o >> 2) << 2), (int)pwin);
+            lb = w >> ((o & 3u) << 3);
+          } else {
+            lb = src.u8(clamp1(seq_anchor + da));
+          }
+        }
         const uint32_t head = ((min(vlit, kRunMask) << 4) | min(vml, kMlMask)) | (remL << 8);
         const uint32_t tail = moff | (remM << 16);
         const uint32_t d = da - vlit;                 // lane - b

@@ -1,8 +1,17 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_selftest.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r03_n2_tests.log 2>&1 || { tail -30 gpurun_out/r03_n2_tests.log; exit 1; }
-tail -2 gpurun_out/r03_n2_tests.log
-timeout -k 10 300 python tools/ab.py kingdb_amd/libkdb_lz4.so --no-headline --reps 3 --uniform 65536:128 --uniform 65536:256 --uniform 65536:512 --uniform 65536:768 --uniform 65536:1024 --uniform 65536:1536 --uniform 65536:2560 --uniform 16384:2560 --uniform 16384:1024 --uniform 16384:512 > gpurun_out/r03_n2_curve.txt 2>&1 || { tail gpurun_out/r03_n2_curve.txt; exit 1; }
-cat gpurun_out/r03_n2_curve.txt
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/r03_n2_quick.json 2> gpurun_out/r03_n2_quick.err || exit 1
-tail -1 gpurun_out/r03_n2_quick.json | cut -c1-400
+O=gpurun_out/r03_n5
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_digests.py tests/test_gpu_hardening.py -x -q -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 || { tail -30 ${O}_tests.log; exit 1; }
+tail -2 ${O}_tests.log
+for v in win base; do
+  timeout -k 10 300 python tools/ab.py kingdb_amd/var/var_$v.so --mixed --reps 5 --uniform 65536:10000 --uniform 16384:40000 --uniform 1048576:600 > ${O}_ab_$v.txt 2>&1 || { tail ${O}_ab_$v.txt; exit 1; }
+  cat ${O}_ab_$v.txt
+done
+for i in 1 2; do
+  for b in kingdb_ref kingdb_hook; do
+    d=/tmp/ce_${b}_$i; rm -rf $d; mkdir -p $d; cd $d
+    KDB_LZ4_FLUSH_STATS=1 timeout -k 10 120 $GRAFT_REPO_ROOT/oracle/_ref/$b/client_emb > $GRAFT_REPO_ROOT/${O}_ce_${b}_$i.txt 2>&1 || { cd $GRAFT_REPO_ROOT; tail ${O}_ce_${b}_$i.txt; exit 1; }
+    cd $GRAFT_REPO_ROOT; rm -rf $d
+    echo "$b $i: $(grep -E 'done in|lz4_flush_stats' ${O}_ce_${b}_$i.txt | tr '\n' ' ')"
+  done
+done
