@@ -163,22 +163,30 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       // window slack for any token; a sequence that fails the test never
       // uses it), so both tests are one scalar decision.
       uint32_t v = lds_rd32_at((uint32_t)als);
-#pragma unroll 1
-      for (;;) {
-        const int mn = (int)(sq & 0xffu) & (int)kMlMask;
-        const int slit = unii(lit);
-        const int aopl = aop + lit;
+      // The sequence's match half and the fast-path test; evaluated before
+      // the loop and at the end of each pass, so the loop is a do-while on
+      // one scalar compare (a mid-loop break had the structurizer carry an
+      // exit flag around the loop: 4 scalar instructions per sequence).
+      int mn, slit, aopl, off, mx, xm, mlen, aref, tst;
+      auto eval = [&]() {
+        mn = (int)(sq & 0xffu) & (int)kMlMask;
+        slit = unii(lit);
+        aopl = aop + lit;
         const uint32_t w = readlane(v, (uint32_t)slit & 63u);   // offset, match-length byte
         const int e = (int)((w >> 16) & 0xffu);
-        const int off = (int)(w & 0xffffu);
-        const int mx = (mn + 1) >> 4;                             // a match-length byte follows
-        const int xm = e & -mx;
-        const int mlen = mn + xm + (int)kMinMatch;
-        const int aref = aopl - off;
+        off = (int)(w & 0xffffu);
+        mx = (mn + 1) >> 4;                                      // a match-length byte follows
+        xm = e & -mx;
+        mlen = mn + xm + (int)kMinMatch;
+        aref = aopl - off;
         // far from both ends, <= 60 literals, ref >= 0, one match-length byte
-        if ((unii((iend8_l - als - lit) | (oexit_l - aopl) | (45 - xl) | (aref - obl) | ((oend5_l - mlen) - aopl)) |
-             (254 - xm)) < 0)
-          break;
+        tst = unii((iend8_l - als - lit) | (oexit_l - aopl) | (45 - xl) | (aref - obl) | ((oend5_l - mlen) - aopl)) |
+              (254 - xm);
+      };
+      eval();
+      if (tst >= 0) {
+#pragma unroll 1
+      do {
         ((lds_b*)(uintptr_t)(uint32_t)aop)[0] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
         const int nt = slit + 2 + mx;                             // next token's lane (<= 63)
         sq = readlane(v, (uint32_t)nt);
@@ -222,6 +230,8 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         }
         asm volatile("" ::: "memory");
         aop = aopl + mlen;
+        eval();
+      } while (tst >= 0);
       }
       ip = unii(avip) - (int)in_abs;
       op = unii(aop) - ob;
