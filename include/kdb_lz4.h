@@ -77,6 +77,9 @@ int kdb_lz4_event_destroy(void* event);
 int kdb_lz4_event_record(void* event, void* stream);
 int kdb_lz4_event_sync(void* event);
 int kdb_lz4_event_elapsed_ms(void* start, void* stop, float* ms);
+/* later work on `stream` waits for `event` (hipStreamWaitEvent): copies on their own
+ * streams behind a kernel, so the two PCIe directions overlap (kingdb_amd/hostpipe.py) */
+int kdb_lz4_stream_wait_event(void* stream, void* event);
 
 /* ------------------------------------------------ scalar LZ4 r1.3.0 mirrors
  * Host buffers, synchronous, one value per call (a batch of one on the GPU).

@@ -54,6 +54,7 @@ SIGNATURES = {
     "kdb_lz4_event_destroy": (_i, [_vp]),
     "kdb_lz4_event_record": (_i, [_vp, _vp]),
     "kdb_lz4_event_sync": (_i, [_vp]),
+    "kdb_lz4_stream_wait_event": (_i, [_vp, _vp]),
     "kdb_lz4_event_elapsed_ms": (_i, [_vp, _vp, _c.POINTER(_c.c_float)]),
     "kdb_lz4_compressBound": (_i, [_i]),
     "kdb_lz4_compress_limitedOutput": (_i, [_c.c_char_p, _vp, _i, _i]),

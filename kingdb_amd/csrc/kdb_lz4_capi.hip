@@ -283,6 +283,9 @@ int kdb_lz4_event_record(void* event, void* stream) {
   return hip_status(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
 }
 int kdb_lz4_event_sync(void* event) { return hip_status(hipEventSynchronize((hipEvent_t)event)); }
+int kdb_lz4_stream_wait_event(void* stream, void* event) {
+  return event ? hip_status(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0)) : KDB_LZ4_EINVAL;
+}
 int kdb_lz4_event_elapsed_ms(void* start, void* stop, float* ms) {
   return ms ? hip_status(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop)) : KDB_LZ4_EINVAL;
 }

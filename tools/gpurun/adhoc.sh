@@ -1,9 +1,11 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-O=gpurun_out/r03_n7
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_digests.py tests/test_gpu_hardening.py -x -q -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 || { tail -30 ${O}_tests.log; exit 1; }
+O=gpurun_out/r03_n9
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_digests.py tests/test_gpu_hardening.py tests/test_capi.py -x -q -m gpu --timeout 120 --timeout-method thread > ${O}_tests.log 2>&1 || { tail -30 ${O}_tests.log; exit 1; }
 tail -2 ${O}_tests.log
-for v in dloop win dloop win; do
+for v in lead cur lead cur; do
   timeout -k 10 300 python tools/ab.py kingdb_amd/var/var_$v.so --mixed --reps 7 --exact-max-in > ${O}_ab_$v.txt 2>&1 || { tail ${O}_ab_$v.txt; exit 1; }
   cat ${O}_ab_$v.txt
 done
+timeout -k 10 600 python bench.py --host-inclusive > ${O}_bench.json 2> ${O}_bench.err || { tail ${O}_bench.err; exit 1; }
+python -c "import json;d=json.loads(open('${O}_bench.json').read().strip().splitlines()[-1]);print(d['value'],d['kernels_ms']);h=d['host_inclusive'];print(h['value'],h['compress_gibs'],h['decompress_gibs']);print(json.dumps(h['stall_profile']))"
