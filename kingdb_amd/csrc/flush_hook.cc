@@ -26,6 +26,7 @@
 
 #include "algorithm/compressor.h"
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -146,16 +147,40 @@ class StagingPool {
   std::vector<Entry> free_;
 };
 
+// One queued PutPartValidSize call.  Its key and (small) chunk bytes were
+// copied by the client thread into that thread's intake arena (below), so the
+// queue holds plain pointers: no shared_ptr of the caller's ByteArrays is
+// copied here and released on the worker (a cross-core cache-line transfer
+// per put), and the caller's own value buffer is freed on the caller's thread,
+// as in the reference.  A chunk over kInlineMax bytes is referenced instead
+// (hold), not copied.
 struct Intake {
   std::thread::id tid;
-  ByteArray key, chunk;
+  const char* kp;
+  const char* cp;
+  uint64_t kn, cn;
   uint64_t offset_chunk, size_value;
+  ByteArray hold;
 };
+constexpr uint64_t kInlineMax = 4096;          // chunks copied into the intake arena
+constexpr uint64_t kArenaBytes = 1ull << 20;    // one intake arena block
+
+// A client thread's current intake arena block.  Order chunks are slices of
+// it (CompressorLZ4::Slice), so the block lives while any of them sits in the
+// write buffer; every batch that has intakes in it also holds it (Pipeline::
+// intake_blocks_), so the worker can read it whatever the orders do.
+struct IntakeArena {
+  uint64_t owner = 0;        // Pipeline::id_
+  uint64_t gen = ~0ull;      // the owner's batch generation it was last registered with
+  ByteArray blk;
+  char* base = nullptr;
+  uint64_t used = 0, cap = 0;
+};
+thread_local IntakeArena t_arena;
+std::atomic<uint64_t> g_pipeline_ids{1};
 
 struct Result {
   ByteArray chunk_final;   // KDB_FLUSH_FRAME / KDB_FLUSH_DISABLED: a slice of the batch's arena
-  ByteArray raw;           // the raw chunk, held until the result is dropped by the worker, so
-                           // that completing an order never frees it on the flush thread
   uint64_t occ = 0, svc = 0;
   uint32_t crc = 0;
   uint8_t mode = KDB_FLUSH_RAW;
@@ -216,16 +241,48 @@ class Pipeline {
               stats_.wait_ms, stats_.complete_ms, ms_since(t0), defer_ns_.load() / 1e6);
   }
 
-  Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket) {
+  Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket,
+               ByteArray* staged) {
     bool kick;
     const Clock::time_point t0 = stats_.on ? Clock::now() : Clock::time_point();
+    const uint64_t kn = key.size(), cn = chunk.size();
+    const bool inline_chunk = cn <= kInlineMax;
+    const uint64_t need = kn + (inline_chunk ? cn : 0);
+    IntakeArena& a = t_arena;
+    if (a.owner != id_ || a.used + need > a.cap) {
+      const uint64_t cap = std::max(kArenaBytes, need);
+      char* p = new char[cap];
+      a.blk = NewShallowCopyByteArray(p, cap);
+      a.base = p;
+      a.used = 0;
+      a.cap = cap;
+      a.owner = id_;
+      a.gen = ~0ull;
+    }
+    char* kp = a.base + a.used;
+    memcpy(kp, key.data(), kn);
+    const char* cp;
+    if (inline_chunk) {
+      memcpy(kp + kn, chunk.data(), cn);
+      cp = kp + kn;
+      *staged = CompressorLZ4::Slice(a.blk, a.used + kn, cn);
+    } else {
+      cp = chunk.data();
+      *staged = chunk;
+    }
+    a.used += need;
     {
       std::lock_guard<std::mutex> l(mu_);
       if (failed_) return Status::IOError("LZ4 flush pipeline failed", failure_);
       *ticket = (uint32_t)next_ticket_++;
       if (intake_.empty()) intake_since_ = std::chrono::steady_clock::now();
-      intake_.push_back(Intake{std::this_thread::get_id(), key, chunk, offset_chunk, size_value});
-      intake_bytes_ += chunk.size();
+      if (a.gen != gen_) {
+        intake_blocks_.push_back(a.blk);
+        a.gen = gen_;
+      }
+      intake_.push_back(Intake{std::this_thread::get_id(), kp, cp, kn, cn, offset_chunk, size_value,
+                               inline_chunk ? ByteArray() : chunk});
+      intake_bytes_ += cn;
       kick = intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts;
     }
     if (kick) cv_work_.notify_one();
@@ -261,11 +318,14 @@ class Pipeline {
   uint64_t full_ticket(uint32_t t) const { return res_base_ + (uint32_t)(t - (uint32_t)res_base_); }
 
   const int device_;
+  const uint64_t id_ = g_pipeline_ids.fetch_add(1);
   std::thread worker_;
   // intake (client threads, worker)
   std::mutex mu_;
   std::condition_variable cv_work_, cv_done_;
   std::vector<Intake> intake_;
+  std::vector<ByteArray> intake_blocks_;   // the arena blocks intake_'s bytes live in
+  uint64_t gen_ = 0;                       // batches taken so far
   uint64_t intake_bytes_ = 0;
   std::chrono::steady_clock::time_point intake_since_;
   uint64_t next_ticket_ = 1;
@@ -291,6 +351,7 @@ void Pipeline::run() {
   kdb_lz4_set_device(device_);
   StagingPool::get().take(device_, stg_);
   std::vector<Intake> batch;
+  std::vector<ByteArray> blocks;
   for (;;) {
     uint64_t t0;
     {
@@ -321,11 +382,14 @@ void Pipeline::run() {
         cv_work_.wait_until(lk, intake_since_ + kBatchAge);
       }
       batch.swap(intake_);
+      blocks.swap(intake_blocks_);
+      gen_++;
       intake_bytes_ = 0;
       t0 = processed_;
     }
     process(batch, t0);   // publishes the results, then processed_
     batch.clear();
+    blocks.clear();
   }
 }
 
@@ -386,7 +450,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     // (consecutive parts mostly come from one thread: skip the hash lookup)
     auto it = (last_it != cur.end() && e.tid == last_tid) ? last_it : cur.find(e.tid);
     const bool fresh = e.offset_chunk == 0;
-    if (it == cur.end() || (fresh && e.chunk.size_const() > 0)) {
+    if (it == cur.end() || (fresh && e.cn > 0)) {
       const bool seen = it != cur.end();
       const uint32_t r = (uint32_t)run_tid.size();
       run_tid.push_back(e.tid);
@@ -439,9 +503,9 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   // ---- staging: host [meta | keys | chunks], device [same | scratch | outputs | frames]
   uint64_t key_bytes = 0, raw_bytes = 0, frame_cap = 0;
   uint32_t max_chunk = 0;
-  for (uint32_t s = 0; s < nseg; s++) key_bytes += batch[seg_head[seg_order[s]]].key.size();
+  for (uint32_t s = 0; s < nseg; s++) key_bytes += batch[seg_head[seg_order[s]]].kn;
   for (uint32_t i = 0; i < m; i++) {
-    const uint64_t c = batch[i].chunk.size();
+    const uint64_t c = batch[i].cn;
     if (c > 0x7E000000ull) return KDB_LZ4_EUNSUPPORTED;
     raw_bytes += c;
     frame_cap += (8 + kdb_lz4_compressBound((int)c) + 15) & ~15ull;
@@ -468,20 +532,20 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   {
     uint64_t ko = 0, co = 0;
     for (uint32_t s = 0; s < nseg; s++) {
-      const ByteArray& k = batch[seg_head[seg_order[s]]].key;
+      const Intake& k = batch[seg_head[seg_order[s]]];
       H64(o_key_off)[s] = ko;
-      H32(o_key_len)[s] = (uint32_t)k.size_const();
-      memcpy(hb + o_keys + ko, k.data_const(), k.size_const());
-      ko += k.size_const();
+      H32(o_key_len)[s] = (uint32_t)k.kn;
+      memcpy(hb + o_keys + ko, k.kp, k.kn);
+      ko += k.kn;
     }
     for (uint32_t q = 0; q < m; q++) {
       const Intake& e = batch[perm[q]];
-      const uint64_t c = e.chunk.size_const();
+      const uint64_t c = e.cn;
       H64(o_chunk_off)[q] = co;
       H32(o_chunk_len)[q] = (uint32_t)c;
       H64(o_offset)[q] = e.offset_chunk;
       H64(o_size)[q] = e.size_value;
-      memcpy(hb + o_chunks + co, e.chunk.data_const(), c);
+      memcpy(hb + o_chunks + co, e.cp, c);
       co += c;
     }
     memcpy(H32(o_seg_first), seg_first.data(), 4ull * (nseg + 1));
@@ -538,7 +602,6 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     r.crc = P.crc;
     r.mode = (uint8_t)P.mode;
     r.status = P.status == 0 ? 0 : -1;
-    r.raw = e.chunk;
     if (r.status) continue;
     if (P.mode == KDB_FLUSH_FRAME) {
       if (P.frame_at + P.size > total) return KDB_LZ4_EHIP;
@@ -546,7 +609,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     } else if (P.mode == KDB_FLUSH_DISABLED) {             // database.cc:201-206
       char* b = arena.data() + dis_at;
       memset(b, 0, 8);
-      memcpy(b + 8, e.chunk.data(), P.size - 8);
+      memcpy(b + 8, e.cp, P.size - 8);
       r.chunk_final = CompressorLZ4::Slice(arena, dis_at, P.size);
       dis_at += P.size;
     }
@@ -556,7 +619,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   {  // what the batch's chunks take in the buffer once final, per raw byte
     uint64_t acc = 0;
     for (uint32_t q = 0; q < m; q++)
-      acc += parts[q].status == 0 && parts[q].mode != KDB_FLUSH_RAW ? parts[q].size : batch[perm[q]].chunk.size();
+      acc += parts[q].status == 0 && parts[q].mode != KDB_FLUSH_RAW ? parts[q].size : batch[perm[q]].cn;
     if (raw_bytes) ratio_q16_.store(std::min<uint64_t>((acc << 16) / raw_bytes, 1u << 17), std::memory_order_relaxed);
   }
   stats_.batches++;
@@ -683,7 +746,7 @@ std::shared_ptr<Pipeline> pipeline_of(const void* wb, bool create) {
 }  // namespace
 
 Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArray& key, ByteArray& chunk,
-                     uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket) {
+                     uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket, ByteArray* staged_chunk) {
   (void)db_options;
   thread_local const void* t_wb = nullptr;
   thread_local std::weak_ptr<Pipeline> t_pipe;
@@ -694,7 +757,7 @@ Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArra
     t_wb = wb;
     t_pipe = p;
   }
-  const Status s = p->defer(key, chunk, offset_chunk, size_value, ticket);
+  const Status s = p->defer(key, chunk, offset_chunk, size_value, ticket, staged_chunk);
   if (s.IsOK()) {
     t_account_raw = chunk.size();
     t_account = p->accounted(chunk.size());

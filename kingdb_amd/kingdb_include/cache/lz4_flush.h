@@ -47,11 +47,13 @@ inline bool LZ4FlushDeferrable(const DatabaseOptions& db_options) {
 }
 
 // Client thread.  Queues one PutPartValidSize call; *ticket goes into the
-// order's crc32 field.  IOError once the pipeline has failed for good (a GPU
-// batch that failed twice): the write is refused, as the reference refuses a
-// put whose compression fails (database.cc:189).
+// order's crc32 field, and *staged_chunk is what goes to WriteBuffer::PutPart:
+// the same bytes, copied into the pipeline's intake arena (chunks up to 4
+// KiB) or the caller's chunk itself.  IOError once the pipeline has failed
+// for good (a GPU batch that failed twice): the write is refused, as the
+// reference refuses a put whose compression fails (database.cc:189).
 Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArray& key, ByteArray& chunk,
-                     uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket);
+                     uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket, ByteArray* staged_chunk);
 // The order of `ticket` never reached the buffer (WriteBuffer::PutPart failed).
 void LZ4FlushCancel(const void* wb, uint32_t ticket);
 // WriteBuffer::WritePart, same client thread, right after LZ4FlushDefer: the

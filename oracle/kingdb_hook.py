@@ -105,9 +105,10 @@ EDITS = {
          "    // frame, offsets, size_value_compressed and CRC32C at the flush (LZ4FlushOrders);\n"
          "    // the order carries its ticket in the crc32 field until then\n"
          "    uint32_t lz4_ticket = 0;\n"
-         "    s = LZ4FlushDefer(wb_, db_options_, key, chunk, offset_chunk, size_value, &lz4_ticket);\n"
+         "    ByteArray lz4_chunk;\n"
+         "    s = LZ4FlushDefer(wb_, db_options_, key, chunk, offset_chunk, size_value, &lz4_ticket, &lz4_chunk);\n"
          "    if (!s.IsOK()) return s;\n"
-         "    s = wb_->PutPart(write_options, key, chunk, offset_chunk, size_value, 0, lz4_ticket);\n"
+         "    s = wb_->PutPart(write_options, key, lz4_chunk, offset_chunk, size_value, 0, lz4_ticket);\n"
          "    if (!s.IsOK()) LZ4FlushCancel(wb_, lz4_ticket);\n"
          "    return s;\n"
          "  }\n"
