@@ -155,31 +155,6 @@ struct Table12 {
 #endif
     return (__builtin_amdgcn_ubfe(oh, s.sh, 4) << 8) | __builtin_amdgcn_ubfe(ol, sl, 8);
   }
-  // The lead chunk's exchange with the puts of EVERY lane but a dead one
-  // (klo/khi = 0xff/15, or 0 for lane 1): a lane past the search bound puts
-  // too.  Such lanes come after every valid lane (and so after the matching
-  // one), so the restore below undoes their puts like any lane's after the
-  // match; p is clamped to 4095, which exceeds every match position (<= S - 12),
-  // so a later lane that reads it never restores it.  With no match the
-  // value's parse ends and its table is discarded.  Saves the valid-lane
-  // compare and the two mask selects per sequence.
-  __device__ __forceinline__ uint32_t xchg_lead(uint32_t h, uint32_t p, uint32_t klo, uint32_t khi, Slot& s) const {
-    const uint32_t sl = (h & 3u) << 3;
-    s.sh = (h & 7u) << 2;
-    s.lo = h;
-    s.hi = (h >> 1) & ~3u;
-    const uint32_t ml = klo << sl;
-    s.mh = khi << s.sh;
-    uint32_t ol, oh;
-    asm volatile(
-        "ds_mskor_rtn_b32 %0, %2, %3, %4 offset:" KDB_STR(KDB_T12_LO) "\n\t"
-        "ds_mskor_rtn_b32 %1, %5, %6, %7 offset:" KDB_STR(KDB_T12_HI) "\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(ol), "=&v"(oh)
-        : "v"(h & ~3u), "v"(ml), "v"((p << sl) & ml), "v"(s.hi), "v"(s.mh), "v"(((p >> 8) << s.sh) & s.mh)
-        : "memory");
-    return (__builtin_amdgcn_ubfe(oh, s.sh, 4) << 8) | __builtin_amdgcn_ubfe(ol, sl, 8);
-  }
   // v: a position < 4096; only lanes whose exchange was on (mh = their nibble mask)
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
     ((lds_u8*)(uintptr_t)(s.lo + kT12Lo))[0] = (uint8_t)v;
@@ -204,10 +179,6 @@ struct Table16 {
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
     ((lds_u16*)(uintptr_t)off)[s.h] = (uint16_t)v;
   }
-  // (Table12 only; compress_block never calls this one)
-  __device__ __forceinline__ uint32_t xchg_lead(uint32_t h, uint32_t p, uint32_t klo, uint32_t, Slot& s) const {
-    return xchg(h, p, klo != 0u, s);
-  }
 };
 
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
@@ -221,10 +192,6 @@ struct Table32 {
     return mskor_rtn(off + (h << 2), on ? 0xffffffffu : 0u, on ? p : 0u);
   }
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const { ((lds_u32*)(uintptr_t)off)[s.h] = v; }
-  // (Table12 only; compress_block never calls this one)
-  __device__ __forceinline__ uint32_t xchg_lead(uint32_t h, uint32_t p, uint32_t klo, uint32_t, Slot& s) const {
-    return xchg(h, p, klo != 0u, s);
-  }
 };
 
 // Value bytes staged in LDS (byte i at p[i]).  kUnclamped: a read outside the
@@ -380,10 +347,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // its start is known (at the end of the sequence before), so the read
     // overlaps that sequence's byte store
     typename Src::Word seq0 = src.rd32_issue(clamp4(1u + lane));
-    // the realigned word, made at the END of the sequence that issued the
-    // loads (after its byte store): one loop-carried VGPR instead of the
-    // three of a Word, which the allocator copied at the loop latch
-    uint32_t seqw = Src::word(seq0);
     // In-place values (HBM/L2): a 256-byte register window of the value from
     // each match's start (one dword per lane, loaded with the count's bytes),
     // from which the next sequence's input words and -- one sequence later --
@@ -415,8 +378,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // always valid, lane 1 never; for a match lanes 0 and 1 never
     const int key_put = lane == 1u ? INT32_MAX : (lane == 0u || lane == 2u) ? INT32_MIN : (int)lane;
     const int key_match = lane <= 1u ? INT32_MAX : lane == 2u ? INT32_MIN : (int)lane;
-    // Table12::xchg_lead's field masks: lane 1 (dead) puts nothing
-    const uint32_t klo_lead = lane == 1u ? 0u : 0xffu, khi_lead = lane == 1u ? 0u : 15u;
     // The rest of a sequence once its search found a match (mm: the matching
     // lanes, pk/refk/slot: the chunk's positions, entries and table slots).
     auto finish = [&](uint64_t mm, uint32_t pk, uint32_t refk, const typename Tab::Slot& slot) {
@@ -621,7 +582,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           op = pos + (int)(lit + xl + xm + 3u);
         }
       }
-      seqw = Src::word(seq0);
     };
     auto sequence = [&](auto lead_c) {
       constexpr uint32_t t0 = decltype(lead_c)::value ? 1u : 0u;
@@ -648,21 +608,13 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       const int bound = (int)((t0 ? kbound1 : kbound0) - anchor);
       {
         pk = anchor + 1u - o3 + lane;
-        const uint32_t seq = seqw;
+        vm = __builtin_amdgcn_sicmp(t0 ? key_put : (int)lane, bound, 41 /*SLE*/);
+        const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
+        const uint32_t seq = Src::word(seq0);
         const uint32_t h = hashp<kWide>(seq);
         // get + put of every valid lane at once, in lane order: refk is the
         // entry as the sequential loop's get at this iteration reads it
-        if constexpr (t0 && std::is_same<Tab, Table12>::value) {
-          // lead chunks of LDS-staged <= 4 KiB values: every lane but the dead
-          // one puts (Table12::xchg_lead); a read of a clamped entry (<= 4095)
-          // stays inside LDS and is masked off below
-          vm = 0;
-          refk = tab.xchg_lead(h, min(pk, 4095u), klo_lead, khi_lead, slot);
-        } else {
-          vm = __builtin_amdgcn_sicmp(t0 ? key_put : (int)lane, bound, 41 /*SLE*/);
-          const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);   // my bit of vm, no VALU
-          refk = tab.xchg(h, pk, valid, slot);
-        }
+        refk = tab.xchg(h, pk, valid, slot);
 #if KDB_ABL_DUP_CAND
         {  // attribution build: the candidate word read twice (opaque address, so both loads stay)
           uint32_t r2 = refk;

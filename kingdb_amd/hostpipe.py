@@ -77,14 +77,19 @@ class HostPipeline:
     """n equal-size values of `size` bytes, processed in chunks of `chunk`
     values over `nstreams` streams."""
 
-    def __init__(self, n: int, size: int, chunk: int = 1 << 16, nstreams: int = 4):
+    def __init__(self, n: int, size: int, chunk: int = 1 << 16, nstreams: int = 4, cdrain: int = 4,
+                 ddrain: int = 1):
         self.n, self.size = int(n), int(size)
         self.chunk = max(1, min(int(chunk), self.n))
         self.nchunks = (self.n + self.chunk - 1) // self.chunk
         self.slot = (frame_bound(size) + 15) & ~15
         n = self.n
         self.streams = [Stream() for _ in range(max(1, nstreams))]
-        self.dstreams = [Stream() for _ in range(max(1, nstreams))]     # device-to-host copies
+        # device-to-host copies: compress drains over `cdrain` streams, decompress
+        # over `ddrain` (its D2H, ΣS bytes, is the larger direction: one stream
+        # keeps it back to back)
+        self.dstreams = [Stream() for _ in range(max(1, nstreams, cdrain, ddrain))]
+        self.cdrain, self.ddrain = max(1, cdrain), max(1, ddrain)
         # host side (pinned): raw values, packed frames, decoded values, metadata
         self.h_raw = PinnedBuffer(n * size)
         self.h_frames = PinnedBuffer(n * self.slot)
@@ -144,7 +149,7 @@ class HostPipeline:
         def drain(c: int) -> None:
             nonlocal host_off
             lo, hi = self._range(c)
-            ds = self.dstreams[c % S]
+            ds = self.dstreams[c % self.cdrain]
             _lib.check(L.kdb_lz4_event_sync(done[c].ptr), "event_sync")
             tot = int(self.h_tot.np[8 * c: 8 * c + 8].view(np.uint64)[0])
             e0 = self._mark(ds)
@@ -178,7 +183,7 @@ class HostPipeline:
             self._span("kernel", c, e0, self.streams[c % S])
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_tot.ptr + 8 * c, self.d_tot.ptr + 8 * c, 8, st), "d2h total")
             done[c].record(self.streams[c % S])
-            ds = self.dstreams[c % S].ptr
+            ds = self.dstreams[c % self.cdrain].ptr
             _lib.check(L.kdb_lz4_stream_wait_event(ds, done[c].ptr), "stream_wait_event")
             for base in (4 * lo, 4 * n + 4 * lo):
                 _lib.check(L.kdb_lz4_memcpy_d2h(self.h_cres.ptr + base, self.d_cres.ptr + base, 4 * m, ds),
@@ -236,7 +241,7 @@ class HostPipeline:
                 "decompress_frames_batch")
             self._span("kernel", c, e0, self.streams[c % S])
             kdone[c].record(self.streams[c % S])
-            ds = self.dstreams[c % S]
+            ds = self.dstreams[c % self.ddrain]
             _lib.check(L.kdb_lz4_stream_wait_event(ds.ptr, kdone[c].ptr), "stream_wait_event")
             e0 = self._mark(ds)
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_out.ptr + lo * size, self.d_out.ptr + lo * size, m * size,
