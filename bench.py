@@ -293,8 +293,15 @@ def ref_write_path(keys: np.ndarray, vals: np.ndarray) -> dict | None:
     d = tempfile.mkdtemp(prefix="kdbref")
     try:
         rec.tofile(os.path.join(d, "s.bin"))
-        r = subprocess.run([exe, os.path.join(d, "db"), os.path.join(d, "s.bin")], check=True, capture_output=True,
-                           text=True, timeout=300)
+        try:
+            # the reference's own KingDB can stop making progress (tools/write_path_cmp.py):
+            # bounded, so a stuck baseline cannot take the GPU line down with it
+            r = subprocess.run([exe, os.path.join(d, "db"), os.path.join(d, "s.bin")], check=True,
+                               capture_output=True, text=True, timeout=100)
+        except subprocess.TimeoutExpired:
+            return {"value": None, "unit": "puts/s", "cores": 1, "kind": "reference",
+                    "note": "the reference's write path (oracle/_ref/ref_db) made no progress within 100 s and was "
+                            "killed; no CPU number this run"}
         f = r.stdout.split()
         t_put, t_all = float(f[2]), float(f[5])
     finally:

@@ -103,6 +103,10 @@ def main() -> None:
     ap.add_argument("--builds", default=",".join(BUILDS))
     ap.add_argument("--out", default=None)
     ap.add_argument("--ceiling", action="store_true", help="also run the reference with compression off")
+    ap.add_argument("--timeout", type=float, default=120.0,
+                    help="seconds per run; a run past it is killed and reported as hung (the reference "
+                         "KingDB itself can stop making progress, see mp3072 below)")
+    ap.add_argument("--repeat", type=int, default=1, help="runs of each build per workload")
     a = ap.parse_args()
     rows = []
     for size in a.sizes.split(","):
@@ -127,12 +131,22 @@ def main() -> None:
                 stream(n, 16, vs).tofile(sp)
                 what = f"{n} puts 16 B keys / {vs} B G1 values"
             ref_files = None
-            for b in a.builds.split(","):
+            for b in [x for x in a.builds.split(",") for _ in range(max(1, a.repeat))]:
                 exe = os.path.join(ROOT, "oracle", "_ref", b, "kdb_db")
                 db = os.path.join(d, "db_" + b)
                 t0 = time.perf_counter()
                 env = dict(os.environ, KDB_LZ4_FLUSH_STATS="1") if b == "kingdb_hook" else None
-                r = subprocess.run([exe, db, sp] + args, capture_output=True, text=True, timeout=900, env=env)
+                try:
+                    r = subprocess.run([exe, db, sp] + args, capture_output=True, text=True, timeout=a.timeout,
+                                       env=env)
+                except subprocess.TimeoutExpired as e:
+                    err = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else (e.stderr or "")
+                    row = {"workload": what, "build": b, "hung": True, "killed_after_s": a.timeout,
+                           "stderr_tail": err[-1500:], "dir": os.path.abspath(a.dir)}
+                    print(json.dumps(row), flush=True)
+                    rows.append(row)
+                    shutil.rmtree(db, ignore_errors=True)
+                    continue
                 wall = time.perf_counter() - t0
                 if r.returncode != 0:
                     print(r.stderr[-2000:], file=sys.stderr)
@@ -165,8 +179,11 @@ def main() -> None:
                 exe = os.path.join(ROOT, "oracle", "_ref", "kingdb_ref", "kdb_db")
                 db = os.path.join(d, "db_none")
                 ca = args + [str(1 << 20), str(32 << 20)][len(args):] + ["1", "none"]
-                r = subprocess.run([exe, db, sp] + ca, capture_output=True, text=True, timeout=900)
-                if r.returncode == 0:
+                try:
+                    r = subprocess.run([exe, db, sp] + ca, capture_output=True, text=True, timeout=a.timeout)
+                except subprocess.TimeoutExpired:
+                    r = None
+                if r is not None and r.returncode == 0:
                     f = r.stdout.split()
                     t_put, t_all = float(f[2]), float(f[5])
                     row = {"workload": what, "build": "kingdb_ref, compression off (ceiling)",
