@@ -222,7 +222,15 @@ struct Stats {
 
 class Pipeline {
  public:
-  explicit Pipeline(int device) : device_(device) { worker_ = std::thread(&Pipeline::run, this); }
+  explicit Pipeline(int device) : device_(device) {
+    worker_ = std::thread(&Pipeline::run, this);
+    // KDB_LZ4_FLUSH_WATCH=<s>: a diagnostic thread prints the pipeline's state
+    // every <s> seconds (tickets issued and processed, intake, worker phase,
+    // a flush waiting), so a run that stops making progress shows where
+    const char* w = getenv("KDB_LZ4_FLUSH_WATCH");
+    const long ws = w ? strtol(w, nullptr, 10) : 0;
+    if (ws > 0) watch_ = std::thread(&Pipeline::watch, this, ws);
+  }
   ~Pipeline() {
     const Clock::time_point t0 = Clock::now();
     {
@@ -230,7 +238,9 @@ class Pipeline {
       stop_ = true;
     }
     cv_work_.notify_all();
+    cv_done_.notify_all();
     worker_.join();
+    if (watch_.joinable()) watch_.join();
     if (stats_.on)
       fprintf(stderr,
               "lz4_flush_stats batches %llu parts %llu raw_bytes %llu stage_ms %.2f gpu_ms %.2f results_ms %.2f "
@@ -310,6 +320,7 @@ class Pipeline {
 
  private:
   void run();
+  void watch(long seconds);
   void drop_consumed();
   void process(std::vector<Intake>& batch, uint64_t t0);
   int gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out);
@@ -319,7 +330,9 @@ class Pipeline {
 
   const int device_;
   const uint64_t id_ = g_pipeline_ids.fetch_add(1);
-  std::thread worker_;
+  std::thread worker_, watch_;
+  std::atomic<int> phase_{0};                // worker: 0 waiting for intake, 1 GPU batch, 2 publishing, 3 dropping
+  std::atomic<uint64_t> complete_waits_for_{0};   // a flush waiting for this ticket (0: none)
   // intake (client threads, worker)
   std::mutex mu_;
   std::condition_variable cv_work_, cv_done_;
@@ -360,7 +373,9 @@ void Pipeline::run() {
         if (garbage_) {
           garbage_ = false;
           lk.unlock();
+          phase_.store(3, std::memory_order_relaxed);
           drop_consumed();
+          phase_.store(0, std::memory_order_relaxed);
           lk.lock();
           continue;
         }
@@ -387,9 +402,25 @@ void Pipeline::run() {
       intake_bytes_ = 0;
       t0 = processed_;
     }
+    phase_.store(1, std::memory_order_relaxed);
     process(batch, t0);   // publishes the results, then processed_
+    phase_.store(0, std::memory_order_relaxed);
     batch.clear();
     blocks.clear();
+  }
+}
+
+void Pipeline::watch(long seconds) {
+  std::unique_lock<std::mutex> lk(mu_);
+  while (!stop_) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(seconds);
+    if (cv_done_.wait_until(lk, until, [&] { return stop_; })) break;
+    fprintf(stderr,
+            "lz4_flush_watch pipeline %llu tickets_issued %llu processed_below %llu intake %zu blocks %zu drain %d "
+            "failed %d worker_phase %d flush_waits_for %llu batches %llu\n",
+            (unsigned long long)id_, (unsigned long long)next_ticket_, (unsigned long long)processed_,
+            intake_.size(), intake_blocks_.size(), (int)drain_, (int)failed_, phase_.load(),
+            (unsigned long long)complete_waits_for_.load(), (unsigned long long)stats_.batches);
   }
 }
 
@@ -652,7 +683,9 @@ void Pipeline::complete(std::vector<Order>& orders) {
       const Clock::time_point tw = Clock::now();
       drain_ = true;
       cv_work_.notify_one();
+      complete_waits_for_.store(newest, std::memory_order_relaxed);
       cv_done_.wait(lk, [&] { return processed_ > newest; });
+      complete_waits_for_.store(0, std::memory_order_relaxed);
       stats_.waits++;
       stats_.wait_ms += ms_since(tw);
     }
