@@ -45,6 +45,34 @@
 #include "../../include/kdb_lz4.h"
 #include "util/logger.h"
 
+#ifdef KDB_LZ4_HANG_DUMP
+// Debug builds only (-DKDB_LZ4_HANG_DUMP, CPU model): SIGUSR1 makes every
+// thread print its stack (SIGUSR2 to each task), for a run that stopped.
+#include <dirent.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+static void kdb_dump_one(int) {
+  void* b[64];
+  const int n = backtrace(b, 64);
+  char hdr[64];
+  const int l = snprintf(hdr, sizeof hdr, "---- thread %ld\n", (long)syscall(SYS_gettid));
+  (void)!write(2, hdr, l);
+  backtrace_symbols_fd(b, n, 2);
+}
+static void kdb_dump_all(int) {
+  DIR* d = opendir("/proc/self/task");
+  if (!d) return;
+  while (struct dirent* e = readdir(d)) {
+    if (e->d_name[0] == '.') continue;
+    syscall(SYS_tgkill, getpid(), atol(e->d_name), SIGUSR2);
+    usleep(20000);
+  }
+  closedir(d);
+}
+#endif
+
 namespace kdb {
 
 namespace {
@@ -818,6 +846,10 @@ void LZ4FlushOrders(const void* wb, const DatabaseOptions& db_options, std::vect
 }
 
 LZ4FlushScope::LZ4FlushScope(const void* wb, const DatabaseOptions& db_options) : wb_(wb) {
+#ifdef KDB_LZ4_HANG_DUMP
+  signal(SIGUSR2, kdb_dump_one);
+  signal(SIGUSR1, kdb_dump_all);
+#endif
   {
     std::lock_guard<std::mutex> l(g_mu);
     g_closed.erase(wb);
