@@ -98,6 +98,38 @@ SEQUENTIAL_PEEK = """  LZ4ReadAhead lz4_read_ahead_;
 READ_INCLUDE = '#include "interface/lz4_read.h"\n'
 
 EDITS = {
+    # KingDB's Event::NotifyWait is a bare notify_one: a Close() that comes while
+    # the storage engine's data thread is still in the last flush's index update
+    # is lost, and StorageEngine::Close joins a thread that sleeps forever in
+    # Wait() (measured with this build: ~1 Close in 6).  The hook
+    # build's flush timing lands there far more often than the reference's, so
+    # it carries the fix: the notification is a flag set under the lock, and
+    # Wait() sleeps on the predicate.
+    "thread/event_manager.h": [
+        ("  T Wait() {\n"
+         "    std::unique_lock<std::mutex> lock(mutex_);\n"
+         "    if (!has_data) {\n"
+         "      cv_ready_.wait(lock);\n"
+         "    }\n"
+         "    return data_;\n"
+         "  }\n",
+         "  T Wait() {\n"
+         "    std::unique_lock<std::mutex> lock(mutex_);\n"
+         "    cv_ready_.wait(lock, [this] { return has_data || notified_; });   // (hook build: no lost wake-up)\n"
+         "    return data_;\n"
+         "  }\n"),
+        ("  void NotifyWait() {\n"
+         "    cv_ready_.notify_one();\n"
+         "  }\n",
+         "  void NotifyWait() {\n"
+         "    std::unique_lock<std::mutex> lock(mutex_);\n"
+         "    notified_ = true;\n"
+         "    cv_ready_.notify_one();\n"
+         "  }\n"),
+        ("  bool has_data;\n",
+         "  bool has_data;\n"
+         "  bool notified_ = false;   // NotifyWait() was called (hook build)\n"),
+    ],
     "interface/database.cc": [
         ('#include "interface/database.h"\n', '#include "interface/database.h"\n' + INCLUDE),
         ("  bool do_compression = true;\n  uint64_t size_value_compressed = 0;\n",
