@@ -206,6 +206,15 @@ struct IntakeArena {
 };
 thread_local IntakeArena t_arena;
 std::atomic<uint64_t> g_pipeline_ids{1};
+// KDB_LZ4_FLUSH_STATS: when WriteBuffer::WritePart accounted this thread's last
+// deferred chunk (its lock and buffer-full wait come after that point)
+thread_local std::chrono::steady_clock::time_point t_accounted;
+thread_local bool t_accounted_set = false;
+std::atomic<uint64_t> g_after_account_max_ns{0};
+const bool g_stats_on = [] {
+  const char* e = getenv("KDB_LZ4_FLUSH_STATS");
+  return e && *e && *e != '0';
+}();
 
 struct Result {
   ByteArray chunk_final;   // KDB_FLUSH_FRAME / KDB_FLUSH_DISABLED: a slice of the batch's arena
@@ -241,7 +250,7 @@ inline double ms_since(Clock::time_point t) {
 struct Stats {
   bool on = false;
   uint64_t batches = 0, parts = 0, raw_bytes = 0, flushes = 0, orders = 0, waits = 0;
-  double gpu_ms = 0, stage_ms = 0, results_ms = 0, wait_ms = 0, complete_ms = 0;
+  double gpu_ms = 0, stage_ms = 0, results_ms = 0, wait_ms = 0, complete_ms = 0, init_ms = 0, first_batch_ms = 0;
   Stats() {
     const char* e = getenv("KDB_LZ4_FLUSH_STATS");
     on = e && *e && *e != '0';
@@ -272,17 +281,43 @@ class Pipeline {
     if (stats_.on)
       fprintf(stderr,
               "lz4_flush_stats batches %llu parts %llu raw_bytes %llu stage_ms %.2f gpu_ms %.2f results_ms %.2f "
-              "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f defer_ms %.2f\n",
+              "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f defer_ms %.2f "
+              "client_stalls %llu client_stall_ms %.2f client_max_gap_ms %.2f init_ms %.2f first_batch_ms %.2f "
+              "max_after_account_ms %.2f\n",
               (unsigned long long)stats_.batches, (unsigned long long)stats_.parts,
               (unsigned long long)stats_.raw_bytes, stats_.stage_ms, stats_.gpu_ms, stats_.results_ms,
               (unsigned long long)stats_.flushes, (unsigned long long)stats_.orders, (unsigned long long)stats_.waits,
-              stats_.wait_ms, stats_.complete_ms, ms_since(t0), defer_ns_.load() / 1e6);
+              stats_.wait_ms, stats_.complete_ms, ms_since(t0), defer_ns_.load() / 1e6,
+              (unsigned long long)stalls_.load(), stall_ns_.load() / 1e6, stall_max_ns_.load() / 1e6, stats_.init_ms,
+              stats_.first_batch_ms, g_after_account_max_ns.load() / 1e6);
   }
 
   Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket,
                ByteArray* staged) {
     bool kick;
     const Clock::time_point t0 = stats_.on ? Clock::now() : Clock::time_point();
+    if (stats_.on) {
+      // the client's time between two of its puts: gaps over 1 ms are stalls
+      // outside the hook (a write buffer that blocks, the allocator, ...)
+      thread_local Clock::time_point t_last;
+      thread_local const Pipeline* t_owner = nullptr;
+      if (t_owner == this) {
+        const uint64_t gap = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - t_last).count();
+        if (gap > 1000000u) {
+          stall_ns_.fetch_add(gap, std::memory_order_relaxed);
+          stalls_.fetch_add(1, std::memory_order_relaxed);
+        }
+        uint64_t m = stall_max_ns_.load(std::memory_order_relaxed);
+        while (gap > m && !stall_max_ns_.compare_exchange_weak(m, gap, std::memory_order_relaxed)) {}
+      }
+      t_owner = this;
+      t_last = t0;
+      if (t_accounted_set) {
+        const uint64_t g = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - t_accounted).count();
+        uint64_t mx = g_after_account_max_ns.load(std::memory_order_relaxed);
+        while (g > mx && !g_after_account_max_ns.compare_exchange_weak(mx, g, std::memory_order_relaxed)) {}
+      }
+    }
     const uint64_t kn = key.size(), cn = chunk.size();
     const bool inline_chunk = cn <= kInlineMax;
     const uint64_t need = kn + (inline_chunk ? cn : 0);
@@ -385,12 +420,21 @@ class Pipeline {
   uint64_t attempts_ = 0;
   Stats stats_;
   std::atomic<uint64_t> ratio_q16_{1u << 16};
-  std::atomic<uint64_t> defer_ns_{0};           // client threads' time in defer() (stats only)   // accounted / raw bytes of the last batch, x 2^16
+  std::atomic<uint64_t> defer_ns_{0};           // client threads' time in defer() (stats only)
+  std::atomic<uint64_t> stall_ns_{0}, stalls_{0}, stall_max_ns_{0};   // client gaps > 1 ms between puts   // accounted / raw bytes of the last batch, x 2^16
 };
 
 void Pipeline::run() {
+  const Clock::time_point t_init = Clock::now();
   kdb_lz4_set_device(device_);
   StagingPool::get().take(device_, stg_);
+  // the first batch's staging (pinned host + device) is allocated here, while
+  // the database opens, not under the first puts: until a batch completes,
+  // deferred chunks are accounted at their raw size (LZ4FlushAccount), and a
+  // slow first batch had let 1 M 100-byte puts fill the write buffer on that
+  // prior and block on its flush (client_embedded)
+  if (!stg_.host) (void)stg_.reserve(16ull << 20, 16ull << 20);
+  if (stats_.on) stats_.init_ms = ms_since(t_init);
   std::vector<Intake> batch;
   std::vector<ByteArray> blocks;
   for (;;) {
@@ -681,6 +725,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
       acc += parts[q].status == 0 && parts[q].mode != KDB_FLUSH_RAW ? parts[q].size : batch[perm[q]].cn;
     if (raw_bytes) ratio_q16_.store(std::min<uint64_t>((acc << 16) / raw_bytes, 1u << 17), std::memory_order_relaxed);
   }
+  if (stats_.on && stats_.batches == 0) stats_.first_batch_ms = ms_since(t_start);
   stats_.batches++;
   stats_.parts += m;
   stats_.raw_bytes += raw_bytes;
@@ -830,6 +875,10 @@ Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArra
 uint64_t LZ4FlushAccount(uint64_t chunk_size) {
   const bool mine = t_account_set && t_account_raw == chunk_size;
   t_account_set = false;
+  if (mine && g_stats_on) {
+    t_accounted = std::chrono::steady_clock::now();
+    t_accounted_set = true;
+  }
   return mine ? t_account : chunk_size;
 }
 
