@@ -251,6 +251,17 @@ struct Stats {
   bool on = false;
   uint64_t batches = 0, parts = 0, raw_bytes = 0, flushes = 0, orders = 0, waits = 0;
   double gpu_ms = 0, stage_ms = 0, results_ms = 0, wait_ms = 0, complete_ms = 0, init_ms = 0, first_batch_ms = 0;
+  // the longest single wait / complete() call, and the longest gap between
+  // one complete() ending and the next starting (the rest of a flush pass)
+  double max_wait_ms = 0, max_complete_ms = 0, max_between_ms = 0;
+  Clock::time_point last_complete_end{};
+  bool completed_once = false;
+  // timeline (ms since the pipeline started): each complete() call's start,
+  // duration, orders and whether the flush pass is a sync one, and where the
+  // client's longest gap between puts began
+  struct Pass { double at, ms; size_t orders; bool sync; };
+  std::vector<Pass> passes;
+  Clock::time_point born = Clock::now();
   Stats() {
     const char* e = getenv("KDB_LZ4_FLUSH_STATS");
     on = e && *e && *e != '0';
@@ -283,13 +294,20 @@ class Pipeline {
               "lz4_flush_stats batches %llu parts %llu raw_bytes %llu stage_ms %.2f gpu_ms %.2f results_ms %.2f "
               "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f defer_ms %.2f "
               "client_stalls %llu client_stall_ms %.2f client_max_gap_ms %.2f init_ms %.2f first_batch_ms %.2f "
-              "max_after_account_ms %.2f\n",
+              "max_after_account_ms %.2f max_wait_ms %.2f max_complete_ms %.2f max_between_ms %.2f\n",
               (unsigned long long)stats_.batches, (unsigned long long)stats_.parts,
               (unsigned long long)stats_.raw_bytes, stats_.stage_ms, stats_.gpu_ms, stats_.results_ms,
               (unsigned long long)stats_.flushes, (unsigned long long)stats_.orders, (unsigned long long)stats_.waits,
               stats_.wait_ms, stats_.complete_ms, ms_since(t0), defer_ns_.load() / 1e6,
               (unsigned long long)stalls_.load(), stall_ns_.load() / 1e6, stall_max_ns_.load() / 1e6, stats_.init_ms,
-              stats_.first_batch_ms, g_after_account_max_ns.load() / 1e6);
+              stats_.first_batch_ms, g_after_account_max_ns.load() / 1e6, stats_.max_wait_ms, stats_.max_complete_ms,
+              stats_.max_between_ms);
+    if (stats_.on) {
+      fprintf(stderr, "lz4_flush_timeline client_max_gap_at_ms %.2f", stall_max_at_ns_.load() / 1e6);
+      for (const Stats::Pass& q : stats_.passes)
+        fprintf(stderr, " | pass at %.2f ms %.2f orders %zu sync %d", q.at, q.ms, q.orders, (int)q.sync);
+      fprintf(stderr, "\n");
+    }
   }
 
   Status defer(ByteArray& key, ByteArray& chunk, uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket,
@@ -309,6 +327,10 @@ class Pipeline {
         }
         uint64_t m = stall_max_ns_.load(std::memory_order_relaxed);
         while (gap > m && !stall_max_ns_.compare_exchange_weak(m, gap, std::memory_order_relaxed)) {}
+        if (gap > m)
+          stall_max_at_ns_.store(
+              (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t_last - stats_.born).count(),
+              std::memory_order_relaxed);
       }
       t_owner = this;
       t_last = t0;
@@ -421,7 +443,7 @@ class Pipeline {
   Stats stats_;
   std::atomic<uint64_t> ratio_q16_{1u << 16};
   std::atomic<uint64_t> defer_ns_{0};           // client threads' time in defer() (stats only)
-  std::atomic<uint64_t> stall_ns_{0}, stalls_{0}, stall_max_ns_{0};   // client gaps > 1 ms between puts   // accounted / raw bytes of the last batch, x 2^16
+  std::atomic<uint64_t> stall_ns_{0}, stalls_{0}, stall_max_ns_{0}, stall_max_at_ns_{0};   // client gaps > 1 ms between puts   // accounted / raw bytes of the last batch, x 2^16
 };
 
 void Pipeline::run() {
@@ -760,7 +782,9 @@ void Pipeline::complete(std::vector<Order>& orders) {
       cv_done_.wait(lk, [&] { return processed_ > newest; });
       complete_waits_for_.store(0, std::memory_order_relaxed);
       stats_.waits++;
-      stats_.wait_ms += ms_since(tw);
+      const double w = ms_since(tw);
+      stats_.wait_ms += w;
+      stats_.max_wait_ms = std::max(stats_.max_wait_ms, w);
     }
   }
   std::lock_guard<std::mutex> l(res_mu_);
@@ -797,7 +821,18 @@ void Pipeline::complete(std::vector<Order>& orders) {
   }
   stats_.flushes++;
   stats_.orders += orders.size();
-  stats_.complete_ms += ms_since(t0);
+  const double c = ms_since(t0);
+  stats_.complete_ms += c;
+  stats_.max_complete_ms = std::max(stats_.max_complete_ms, c);
+  if (stats_.completed_once)
+    stats_.max_between_ms = std::max(
+        stats_.max_between_ms,
+        std::chrono::duration<double, std::milli>(t0 - stats_.last_complete_end).count());
+  stats_.last_complete_end = Clock::now();
+  stats_.completed_once = true;
+  if (stats_.on && stats_.passes.size() < 64)
+    stats_.passes.push_back({std::chrono::duration<double, std::milli>(t0 - stats_.born).count(), c, orders.size(),
+                             !orders.empty() && orders[0].write_options.sync});
   // the consumed results are dropped by the worker (drop_consumed), off this thread
   {
     std::lock_guard<std::mutex> l2(mu_);
