@@ -69,10 +69,11 @@ void CRC32LZ4::stream(const char* data, size_t n) {  // crc32c.h:87-92
 }
 
 // compressor.cc:9-12
-void CompressorLZ4::WarmUp() {
-  static std::once_flag once;
-  std::call_once(once, [] { (void)kdb_lz4_warmup(); });   // no device: the calls report it later
-}
+// Per device: kdb_lz4_warmup readies the calling thread's current device once
+// (cached per device inside the library, retried after a failure), so a
+// database opened on another device does not pay its first launches and
+// self-test inside its first puts.  No device: the calls report it later.
+void CompressorLZ4::WarmUp() { (void)kdb_lz4_warmup(); }
 
 void CompressorLZ4::ResetThreadLocalStorage() {
   ts_compress_.reset();

@@ -67,9 +67,10 @@ uint32_t Crc32cExtend(uint32_t crc, const char* data, size_t n);
 
 class CompressorLZ4 {
  public:
-  // The first instance in a process readies the GPU (kdb_lz4_warmup: the
-  // lane-order self-test, the code object, the runtime's first-launch costs),
-  // so a Database pays them when it is built, not in its first puts.
+  // An instance readies its thread's current device (kdb_lz4_warmup, once per
+  // device: the lane-order self-test, the code object, the runtime's
+  // first-launch costs), so a Database pays them when it is built, not in its
+  // first puts.
   CompressorLZ4() { WarmUp(); }
   // compressor.h:110-113: assignment does not copy state.
   CompressorLZ4& operator=(const CompressorLZ4&) { return *this; }

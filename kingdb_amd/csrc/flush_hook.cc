@@ -18,10 +18,22 @@
 //   flush thread     LZ4FlushOrders: waits for the tickets of the buffer being
 //                    flushed (usually long done: the worker runs while the
 //                    buffer fills), then completes each order in place
-// A GPU batch that fails is retried once on a fresh stream and fresh staging;
-// if that fails too its orders are dropped (never written without their frame
-// and checksum), the failure is latched and every later LZ4FlushDefer returns
-// IOError: the process keeps running.
+// The reference's put contract (database.cc:128-276): a put it acknowledges is
+// stored, and a put it refuses gets its IOError at that very call.
+//   * A GPU batch that fails is retried once on a fresh stream and fresh
+//     staging; if that fails too, the batch is completed on the host in the
+//     reference's own disabled-compression form (:199-209: 8 zero bytes + the
+//     raw chunk for the part that switches, the raw chunk for the value's later
+//     parts; offsets, size_value_compressed and the CRC32C as the reference
+//     computes them on that branch) -- no LZ4 runs on the host, and no
+//     acknowledged put is lost.  Each thread's carried state follows it, so the
+//     next batch (GPU again) continues from it.
+//   * The only IOErrors PutPartValidSize can return (:189, :261-266) need a part
+//     outside the regular shape -- a value's parts in order, contiguous from
+//     offset 0, non-empty (see Pipeline::regular) -- so such a part waits for
+//     its own result inside LZ4FlushDefer and returns the reference's status
+//     there, before its order reaches the buffer; regular parts cannot fail and
+//     return at once.
 #include "cache/lz4_flush.h"
 
 #include "algorithm/compressor.h"
@@ -221,9 +233,16 @@ struct Result {
   uint64_t occ = 0, svc = 0;
   uint32_t crc = 0;
   uint8_t mode = KDB_FLUSH_RAW;
-  int8_t status = 0;       // -1: the order is dropped
+  int8_t status = 0;       // -1: PutPartValidSize returns IOError (mode FAILED: :189, else :261-266)
   bool consumed = false;
 };
+
+// database.cc's two IOError statuses of PutPartValidSize
+Status put_status(const Result& r) {
+  if (r.mode == KDB_FLUSH_FAILED) return Status::IOError("LZ4_compress_limitedOutput() failed");   // compressor.cc:33
+  log::emerg("Database::PutPartValidSize()", "Error: write was attempted outside of the allocated memory.");
+  return Status::IOError("Prevented write to occur outside of the allocated memory.");                // :264-265
+}
 
 // KDB_LZ4_FLUSH_INJECT=<first>:<count> -- test knob: GPU batch attempts
 // first .. first+count-1 (counted from 1) fail as a failed
@@ -302,6 +321,10 @@ class Pipeline {
               (unsigned long long)stalls_.load(), stall_ns_.load() / 1e6, stall_max_ns_.load() / 1e6, stats_.init_ms,
               stats_.first_batch_ms, g_after_account_max_ns.load() / 1e6, stats_.max_wait_ms, stats_.max_complete_ms,
               stats_.max_between_ms);
+    if (stats_.on)
+      fprintf(stderr, "lz4_flush_contract settled_parts %llu refused_parts %llu host_batches %llu host_parts %llu\n",
+              (unsigned long long)settles_.load(), (unsigned long long)refused_.load(),
+              (unsigned long long)host_batches_.load(), (unsigned long long)host_parts_.load());
     if (stats_.on) {
       fprintf(stderr, "lz4_flush_timeline client_max_gap_at_ms %.2f", stall_max_at_ns_.load() / 1e6);
       for (const Stats::Pass& q : stats_.passes)
@@ -366,9 +389,11 @@ class Pipeline {
       *staged = chunk;
     }
     a.used += need;
+    const bool settle = !regular(offset_chunk, cn, size_value);
+    uint64_t mine;
     {
       std::lock_guard<std::mutex> l(mu_);
-      if (failed_) return Status::IOError("LZ4 flush pipeline failed", failure_);
+      mine = next_ticket_;
       *ticket = (uint32_t)next_ticket_++;
       if (intake_.empty()) intake_since_ = std::chrono::steady_clock::now();
       if (a.gen != gen_) {
@@ -381,9 +406,76 @@ class Pipeline {
       kick = intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts;
     }
     if (kick) cv_work_.notify_one();
+    Status s = Status::OK();
+    if (settle) s = settle_part(mine);
     if (stats_.on) defer_ns_.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(),
                                        std::memory_order_relaxed);
-    return Status::OK();
+    return s;
+  }
+
+  // Whether this client thread's part has the regular shape, in which
+  // PutPartValidSize cannot fail: a value's first part (offset 0, bytes), or
+  // the next part of the value this thread's last part belongs to (same
+  // size_value, contiguous offset, bytes); an empty value (no bytes, size 0).
+  // Why nothing else is needed (database.cc:143-266, per thread): a first part
+  // with bytes resets the state (:159-162, :177-179); while compression stays
+  // on, a frame F <= chunk + 8 (compressor.cc:40-48) is kept only if the
+  // value's raw rest + 8 still fits behind it (:197-200), so by induction
+  // o + (size_value - offset) + 8 <= size_value + padding before each part, F
+  // never exceeds space_left (no unsigned wrap at :200), and neither a kept
+  // frame nor the part that switches (chunk + 8) nor the raw parts after it
+  // -- contiguous, so they add up to the value's rest -- pass :262; Compress
+  // fails (:189) only above LZ4_MAX_INPUT_SIZE.  Any other part (a gap, an
+  // overlap, parts of two values interleaved on one thread, an empty chunk in
+  // a value, a part after the value's end) is settled synchronously.
+  bool regular(uint64_t offset_chunk, uint64_t cn, uint64_t size_value) {
+    struct Track {
+      uint64_t owner;                // Pipeline::id_
+      bool open;                     // the thread's last part left its value unfinished
+      uint64_t end, size_value;
+    };
+    thread_local Track t = {0, false, 0, 0};
+    if (t.owner != id_) t = Track{id_, false, 0, 0};
+    const bool bytes = cn > 0 && cn <= 0x7E000000ull;
+    bool ok;
+    if (offset_chunk == 0 && bytes) {
+      ok = true;
+      t.end = cn;
+      t.size_value = size_value;
+    } else if (t.open && bytes && offset_chunk == t.end && size_value == t.size_value) {
+      ok = true;
+      t.end += cn;
+    } else {
+      ok = offset_chunk == 0 && cn == 0 && size_value == 0;
+      t.end = 0;
+    }
+    t.open = ok && t.end < size_value;
+    return ok;
+  }
+
+  // An irregular part waits for its own result (the worker is asked to take
+  // the intake at once) and returns PutPartValidSize's status; a refused
+  // part's result is dropped here, as its order never reaches the buffer.
+  Status settle_part(uint64_t mine) {
+    settles_.fetch_add(1, std::memory_order_relaxed);
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      if (processed_ <= mine) {
+        drain_ = true;
+        cv_work_.notify_one();
+        cv_done_.wait(lk, [&] { return processed_ > mine; });
+      }
+    }
+    Result r0;
+    {
+      std::lock_guard<std::mutex> l(res_mu_);
+      const uint64_t at = mine - res_base_;   // not consumed (no order holds it yet), so still queued
+      if (at >= res_.size() || res_[at].status == 0) return Status::OK();
+      r0.mode = res_[at].mode;
+      cancelled_.insert((uint32_t)mine);
+    }
+    refused_.fetch_add(1, std::memory_order_relaxed);
+    return put_status(r0);
   }
 
   void cancel(uint32_t ticket) {
@@ -409,6 +501,7 @@ class Pipeline {
   void drop_consumed();
   void process(std::vector<Intake>& batch, uint64_t t0);
   int gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out);
+  void host_batch(std::vector<Intake>& batch, std::vector<Result>& out);
 
   // the 64-bit ticket of an order's 32 bits (outstanding tickets span < 2^32)
   uint64_t full_ticket(uint32_t t) const { return res_base_ + (uint32_t)(t - (uint32_t)res_base_); }
@@ -428,8 +521,7 @@ class Pipeline {
   std::chrono::steady_clock::time_point intake_since_;
   uint64_t next_ticket_ = 1;
   uint64_t processed_ = 1;           // tickets below have results
-  bool drain_ = false, stop_ = false, failed_ = false, garbage_ = false;
-  std::string failure_;
+  bool drain_ = false, stop_ = false, garbage_ = false;
   // results (worker appends, flush thread consumes)
   std::mutex res_mu_;
   std::deque<Result> res_;
@@ -439,16 +531,26 @@ class Pipeline {
   std::unordered_map<std::thread::id, kdb_flush_state> state_;
   Staging stg_;
   Inject inject_;
+  // KDB_LZ4_FLUSH_MAX_PARTS=<n> -- test knob: at most n parts per GPU batch, so
+  // a small stream's multipart values straddle batches (tests/test_hook_contract.py)
+  const size_t max_parts_ = [] {
+    const char* e = getenv("KDB_LZ4_FLUSH_MAX_PARTS");
+    return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
+  }();
   uint64_t attempts_ = 0;
   Stats stats_;
   std::atomic<uint64_t> ratio_q16_{1u << 16};
   std::atomic<uint64_t> defer_ns_{0};           // client threads' time in defer() (stats only)
+  std::atomic<uint64_t> settles_{0}, refused_{0};   // irregular parts settled in defer(), and refused there
+  std::atomic<uint64_t> host_batches_{0}, host_parts_{0};
+  std::atomic<uint64_t> gpu_batches_{0};   // batches completed on the host (GPU failed twice)
   std::atomic<uint64_t> stall_ns_{0}, stalls_{0}, stall_max_ns_{0}, stall_max_at_ns_{0};   // client gaps > 1 ms between puts   // accounted / raw bytes of the last batch, x 2^16
 };
 
 void Pipeline::run() {
   const Clock::time_point t_init = Clock::now();
   kdb_lz4_set_device(device_);
+  (void)kdb_lz4_warmup();   // this device's first launches, once per device
   StagingPool::get().take(device_, stg_);
   // the first batch's staging (pinned host + device) is allocated here, while
   // the database opens, not under the first puts: until a batch completes,
@@ -490,10 +592,19 @@ void Pipeline::run() {
           break;
         cv_work_.wait_until(lk, intake_since_ + kBatchAge);
       }
-      batch.swap(intake_);
-      blocks.swap(intake_blocks_);
+      if (max_parts_ && intake_.size() > max_parts_) {   // (test knob: the rest stays queued)
+        batch.assign(std::make_move_iterator(intake_.begin()), std::make_move_iterator(intake_.begin() + (long)max_parts_));
+        intake_.erase(intake_.begin(), intake_.begin() + (long)max_parts_);
+        blocks = intake_blocks_;                           // (the rest's arena blocks stay registered too)
+        intake_bytes_ = 0;
+        for (const Intake& e : intake_) intake_bytes_ += e.cn;
+        intake_since_ = std::chrono::steady_clock::now();
+      } else {
+        batch.swap(intake_);
+        blocks.swap(intake_blocks_);
+        intake_bytes_ = 0;
+      }
       gen_++;
-      intake_bytes_ = 0;
       t0 = processed_;
     }
     phase_.store(1, std::memory_order_relaxed);
@@ -511,10 +622,10 @@ void Pipeline::watch(long seconds) {
     if (cv_done_.wait_until(lk, until, [&] { return stop_; })) break;
     fprintf(stderr,
             "lz4_flush_watch pipeline %llu tickets_issued %llu processed_below %llu intake %zu blocks %zu drain %d "
-            "failed %d worker_phase %d flush_waits_for %llu batches %llu\n",
+            "host_batches %llu worker_phase %d flush_waits_for %llu batches %llu\n",
             (unsigned long long)id_, (unsigned long long)next_ticket_, (unsigned long long)processed_,
-            intake_.size(), intake_blocks_.size(), (int)drain_, (int)failed_, phase_.load(),
-            (unsigned long long)complete_waits_for_.load(), (unsigned long long)stats_.batches);
+            intake_.size(), intake_blocks_.size(), (int)drain_, (unsigned long long)host_batches_.load(),
+            phase_.load(), (unsigned long long)complete_waits_for_.load(), (unsigned long long)gpu_batches_.load());
   }
 }
 
@@ -526,15 +637,11 @@ void Pipeline::process(std::vector<Intake>& batch, uint64_t t0) {
     stg_.drop();
     rc = gpu_batch(batch, out);
   }
-  std::string why;
   if (rc != KDB_LZ4_OK) {
-    why = "GPU batch failed twice (" + std::to_string(rc) + ")";
-    log::emerg("LZ4FlushPipeline", "%s: %zu parts dropped", why.c_str(), batch.size());
+    log::emerg("LZ4FlushPipeline", "GPU batch failed twice (%d): %zu parts stored uncompressed", rc, batch.size());
     stg_.drop();
-    for (Result& r : out) {
-      r = Result();
-      r.status = -1;
-    }
+    for (Result& r : out) r = Result();
+    host_batch(batch, out);
   }
   {
     std::lock_guard<std::mutex> l(res_mu_);
@@ -543,12 +650,69 @@ void Pipeline::process(std::vector<Intake>& batch, uint64_t t0) {
   {
     std::lock_guard<std::mutex> l(mu_);
     processed_ = t0 + batch.size();
-    if (!why.empty() && !failed_) {
-      failed_ = true;
-      failure_ = why;
-    }
   }
   cv_done_.notify_all();
+}
+
+// A batch the GPU could not run (twice), completed on the host exactly as
+// PutPartValidSize completes parts whose compression is switched off
+// (database.cc:143-266 with the :199 test taken): the first compressed part of
+// a value becomes 8 zero bytes + its chunk (:200-208), later parts stay raw
+// (:164-174), offsets / size_value_compressed / the CRC32C follow those
+// branches (:237-257) and the :261-266 check is made.  Every acknowledged put
+// is stored (readable by the reference's UncompressByteArray, compressor.cc:
+// 173-180, 213-245); each thread's carried state is the reference's after the
+// same calls, so a later GPU batch continues from it.  No LZ4 on the host;
+// the CRC32C is the drop-in's host Crc32cExtend (compressor.cc).
+void Pipeline::host_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
+  const uint32_t m = (uint32_t)batch.size();
+  uint64_t dis_bytes = 0;
+  for (const Intake& e : batch) dis_bytes += e.cn + 8;
+  char* a = dis_bytes ? new char[dis_bytes] : nullptr;
+  ByteArray arena = a ? NewShallowCopyByteArray(a, dis_bytes) : ByteArray();
+  uint64_t at = 0;
+  for (uint32_t i = 0; i < m; i++) {
+    const Intake& e = batch[i];
+    Result& r = out[i];
+    kdb_flush_state& S = state_[e.tid];
+    const uint64_t csz = e.cn, off = e.offset_chunk, V = e.size_value;
+    const uint64_t pad = (V / 65536u + 1u) * 8u;                     // format.h:63-71
+    const bool first = off == 0, last = csz + off == V, do_comp = csz != 0;
+    uint64_t o = off, size = csz;
+    r.mode = KDB_FLUSH_RAW;
+    if (first) { S.enabled = 1u; S.ts_offset = 0; }                   // :159-162
+    if (!S.enabled) { o = S.ts_offset; S.ts_offset = o + csz; }        // :164-171
+    if (do_comp && S.enabled) {
+      if (first) S.comp_total = 0;                                    // :177-179
+      o = S.comp_total;                                               // :182
+      if (csz > 0x7E000000ull) {                                      // :185-189 (LZ4_MAX_INPUT_SIZE)
+        r.mode = KDB_FLUSH_FAILED;
+        r.status = -1;
+        r.occ = o;
+        continue;
+      }
+      size = csz + 8u;                                                // :199-209, the test taken
+      S.enabled = 0u;
+      S.ts_offset = S.comp_total + size;
+      r.mode = KDB_FLUSH_DISABLED;
+      memset(a + at, 0, 8);
+      memcpy(a + at + 8, e.cp, csz);
+      r.chunk_final = CompressorLZ4::Slice(arena, at, size);
+      at += size;
+    }
+    if (do_comp && last) r.svc = S.enabled ? S.comp_total : (first ? S.ts_offset : o + csz);   // :237-248
+    if (first) S.crc = Crc32cExtend(0u, e.kp, e.kn);                 // :251-255
+    if (r.mode == KDB_FLUSH_DISABLED) {
+      static const char zeros[8] = {0};
+      S.crc = Crc32cExtend(S.crc, zeros, 8);
+    }
+    S.crc = Crc32cExtend(S.crc, e.cp, csz);                          // :256
+    r.crc = last ? S.crc : 0u;                                        // :257
+    r.occ = o;
+    if (o + size > V + (do_comp ? pad : 0u)) r.status = -1;           // :261-266
+  }
+  host_batches_.fetch_add(1, std::memory_order_relaxed);
+  host_parts_.fetch_add(m, std::memory_order_relaxed);
 }
 
 // The batch through the GPU: layout (segments, runs), staging, one
@@ -749,6 +913,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   }
   if (stats_.on && stats_.batches == 0) stats_.first_batch_ms = ms_since(t_start);
   stats_.batches++;
+  gpu_batches_.fetch_add(1, std::memory_order_relaxed);   // (read by watch(), which holds mu_ only)
   stats_.parts += m;
   stats_.raw_bytes += raw_bytes;
   stats_.stage_ms += t_stage;

@@ -49,9 +49,11 @@ inline bool LZ4FlushDeferrable(const DatabaseOptions& db_options) {
 // Client thread.  Queues one PutPartValidSize call; *ticket goes into the
 // order's crc32 field, and *staged_chunk is what goes to WriteBuffer::PutPart:
 // the same bytes, copied into the pipeline's intake arena (chunks up to 4
-// KiB) or the caller's chunk itself.  IOError once the pipeline has failed
-// for good (a GPU batch that failed twice): the write is refused, as the
-// reference refuses a put whose compression fails (database.cc:189).
+// KiB) or the caller's chunk itself.  Returns what PutPartValidSize returns
+// for this call: a part of the regular shape (a value's parts in order,
+// contiguous from offset 0, non-empty) cannot fail there and returns OK at
+// once; any other part waits for its own result and returns the reference's
+// IOError (database.cc:189, :261-266) at this call, its order never queued.
 Status LZ4FlushDefer(const void* wb, const DatabaseOptions& db_options, ByteArray& key, ByteArray& chunk,
                      uint64_t offset_chunk, uint64_t size_value, uint32_t* ticket, ByteArray* staged_chunk);
 // The order of `ticket` never reached the buffer (WriteBuffer::PutPart failed).
@@ -63,9 +65,11 @@ void LZ4FlushCancel(const void* wb, uint32_t ticket);
 uint64_t LZ4FlushAccount(uint64_t chunk_size);
 
 // Flush thread, buffer readers held off.  Completes every deferred order of
-// `orders` in place; an order whose PutPartValidSize call fails (IOError
-// there, or a GPU batch that failed twice) is removed, so no order reaches an
-// HSTable without its frame and checksum.  Never aborts.
+// `orders` in place (an order without a result of this pipeline is removed,
+// so none reaches an HSTable without its chunk_final and checksum).  A GPU
+// batch that failed twice was completed on the host in the reference's
+// disabled-compression form (database.cc:199-209): every acknowledged put is
+// stored.  Never aborts.
 void LZ4FlushOrders(const void* wb, const DatabaseOptions& db_options, std::vector<Order>& orders);
 
 // ProcessingLoop's local: creates the pipeline (GPU stream, staging, worker
