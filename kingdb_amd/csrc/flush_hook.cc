@@ -201,6 +201,7 @@ struct Intake {
   uint64_t kn, cn;
   uint64_t offset_chunk, size_value;
   ByteArray hold;
+  uint64_t ticket;
 };
 constexpr uint64_t kInlineMax = 4096;          // chunks copied into the intake arena
 constexpr uint64_t kArenaBytes = 1ull << 20;    // one intake arena block
@@ -211,7 +212,8 @@ constexpr uint64_t kArenaBytes = 1ull << 20;    // one intake arena block
 // intake_blocks_), so the worker can read it whatever the orders do.
 struct IntakeArena {
   uint64_t owner = 0;        // Pipeline::id_
-  uint64_t gen = ~0ull;      // the owner's batch generation it was last registered with
+  size_t lane = 0;           // the lane it was last registered with
+  uint64_t gen = ~0ull;      // that lane's batch generation then
   ByteArray blk;
   char* base = nullptr;
   uint64_t used = 0, cap = 0;
@@ -234,6 +236,7 @@ struct Result {
   uint32_t crc = 0;
   uint8_t mode = KDB_FLUSH_RAW;
   int8_t status = 0;       // -1: PutPartValidSize returns IOError (mode FAILED: :189, else :261-266)
+  bool ready = false;      // the lane that took the part has published it
   bool consumed = false;
 };
 
@@ -268,8 +271,8 @@ inline double ms_since(Clock::time_point t) {
 // it stops (tools/write_path_cmp.py --stats).
 struct Stats {
   bool on = false;
-  uint64_t batches = 0, parts = 0, raw_bytes = 0, flushes = 0, orders = 0, waits = 0;
-  double gpu_ms = 0, stage_ms = 0, results_ms = 0, wait_ms = 0, complete_ms = 0, init_ms = 0, first_batch_ms = 0;
+  uint64_t flushes = 0, orders = 0, waits = 0;
+  double wait_ms = 0, complete_ms = 0;
   // the longest single wait / complete() call, and the longest gap between
   // one complete() ending and the next starting (the rest of a flush pass)
   double max_wait_ms = 0, max_complete_ms = 0, max_between_ms = 0;
@@ -287,10 +290,52 @@ struct Stats {
   }
 };
 
+// One device's share of a pipeline: a worker thread bound to the device, its
+// intake, staging and stream, and the carried PutPartValidSize state of the
+// client threads whose parts it takes.  A client thread's parts go to one
+// lane at a time; it moves to the next lane only at a value's first part with
+// bytes, where the reference resets every piece of that state
+// (database.cc:159-162, 177-179, 252-255), so no state crosses lanes.
+struct Lane {
+  int device = 0;
+  size_t index = 0;
+  std::thread worker;
+  std::condition_variable cv_work;          // (with Pipeline::mu_)
+  // intake: client threads and this lane's worker, under Pipeline::mu_
+  std::vector<Intake> intake;
+  std::vector<ByteArray> intake_blocks;     // the arena blocks intake's bytes live in
+  uint64_t gen = 0;                         // batches taken so far
+  uint64_t intake_bytes = 0;
+  Clock::time_point intake_since;
+  bool drain = false;
+  // worker only
+  std::unordered_map<std::thread::id, kdb_flush_state> state;
+  Staging stg;
+  std::atomic<int> phase{0};                // 0 waiting for intake, 1 batch, 3 dropping results
+  // stats (worker; read after it joined)
+  uint64_t batches = 0, parts = 0, raw_bytes = 0;
+  double gpu_ms = 0, stage_ms = 0, results_ms = 0, init_ms = 0, first_batch_ms = 0;
+};
+// bytes a client thread sends to one lane before it moves on (at a value's
+// first part), so even one writer spreads its batches over the devices
+constexpr uint64_t kLaneSpan = 2ull << 20;
+
 class Pipeline {
  public:
   explicit Pipeline(int device) : device_(device) {
-    worker_ = std::thread(&Pipeline::run, this);
+    // the lanes: this thread's device first, then the other visible ones
+    // (KDB_LZ4_FLUSH_DEVICES=<n> caps how many)
+    int count = 1;
+    if (kdb_lz4_device_count(&count) != KDB_LZ4_OK || count < 1) count = 1;
+    const char* cap = getenv("KDB_LZ4_FLUSH_DEVICES");
+    const long want = cap && *cap ? strtol(cap, nullptr, 10) : count;
+    const int n = (int)std::max(1L, std::min<long>(count, want));
+    for (int k = 0; k < n; k++) {
+      lanes_.emplace_back(new Lane());
+      lanes_.back()->device = (device + k) % count;
+      lanes_.back()->index = (size_t)k;
+    }
+    for (auto& L : lanes_) L->worker = std::thread(&Pipeline::run, this, L.get());
     // KDB_LZ4_FLUSH_WATCH=<s>: a diagnostic thread prints the pipeline's state
     // every <s> seconds (tickets issued and processed, intake, worker phase,
     // a flush waiting), so a run that stops making progress shows where
@@ -304,23 +349,42 @@ class Pipeline {
       std::lock_guard<std::mutex> l(mu_);
       stop_ = true;
     }
-    cv_work_.notify_all();
+    for (auto& L : lanes_) L->cv_work.notify_all();
     cv_done_.notify_all();
-    worker_.join();
+    for (auto& L : lanes_) L->worker.join();
     if (watch_.joinable()) watch_.join();
+    Lane sum;
+    for (auto& L : lanes_) {
+      sum.batches += L->batches;
+      sum.parts += L->parts;
+      sum.raw_bytes += L->raw_bytes;
+      sum.gpu_ms += L->gpu_ms;
+      sum.stage_ms += L->stage_ms;
+      sum.results_ms += L->results_ms;
+      sum.init_ms = std::max(sum.init_ms, L->init_ms);
+      if (L->index == 0) sum.first_batch_ms = L->first_batch_ms;
+    }
     if (stats_.on)
       fprintf(stderr,
               "lz4_flush_stats batches %llu parts %llu raw_bytes %llu stage_ms %.2f gpu_ms %.2f results_ms %.2f "
               "flushes %llu orders %llu waits %llu wait_ms %.2f complete_ms %.2f stop_ms %.2f defer_ms %.2f "
               "client_stalls %llu client_stall_ms %.2f client_max_gap_ms %.2f init_ms %.2f first_batch_ms %.2f "
               "max_after_account_ms %.2f max_wait_ms %.2f max_complete_ms %.2f max_between_ms %.2f\n",
-              (unsigned long long)stats_.batches, (unsigned long long)stats_.parts,
-              (unsigned long long)stats_.raw_bytes, stats_.stage_ms, stats_.gpu_ms, stats_.results_ms,
+              (unsigned long long)sum.batches, (unsigned long long)sum.parts,
+              (unsigned long long)sum.raw_bytes, sum.stage_ms, sum.gpu_ms, sum.results_ms,
               (unsigned long long)stats_.flushes, (unsigned long long)stats_.orders, (unsigned long long)stats_.waits,
               stats_.wait_ms, stats_.complete_ms, ms_since(t0), defer_ns_.load() / 1e6,
-              (unsigned long long)stalls_.load(), stall_ns_.load() / 1e6, stall_max_ns_.load() / 1e6, stats_.init_ms,
-              stats_.first_batch_ms, g_after_account_max_ns.load() / 1e6, stats_.max_wait_ms, stats_.max_complete_ms,
+              (unsigned long long)stalls_.load(), stall_ns_.load() / 1e6, stall_max_ns_.load() / 1e6, sum.init_ms,
+              sum.first_batch_ms, g_after_account_max_ns.load() / 1e6, stats_.max_wait_ms, stats_.max_complete_ms,
               stats_.max_between_ms);
+    if (stats_.on) {
+      fprintf(stderr, "lz4_flush_lanes %zu", lanes_.size());
+      for (auto& L : lanes_)
+        fprintf(stderr, " | lane %zu device %d batches %llu parts %llu raw_bytes %llu gpu_ms %.2f", L->index, L->device,
+                (unsigned long long)L->batches, (unsigned long long)L->parts, (unsigned long long)L->raw_bytes,
+                L->gpu_ms);
+      fprintf(stderr, "\n");
+    }
     if (stats_.on)
       fprintf(stderr, "lz4_flush_contract settled_parts %llu refused_parts %llu host_batches %llu host_parts %llu\n",
               (unsigned long long)settles_.load(), (unsigned long long)refused_.load(),
@@ -390,24 +454,26 @@ class Pipeline {
     }
     a.used += need;
     const bool settle = !regular(offset_chunk, cn, size_value);
+    Lane& L = *lanes_[lane_of(offset_chunk, cn)];
     uint64_t mine;
     {
       std::lock_guard<std::mutex> l(mu_);
       mine = next_ticket_;
       *ticket = (uint32_t)next_ticket_++;
-      if (intake_.empty()) intake_since_ = std::chrono::steady_clock::now();
-      if (a.gen != gen_) {
-        intake_blocks_.push_back(a.blk);
-        a.gen = gen_;
+      if (L.intake.empty()) L.intake_since = Clock::now();
+      if (a.lane != L.index || a.gen != L.gen) {
+        L.intake_blocks.push_back(a.blk);
+        a.lane = L.index;
+        a.gen = L.gen;
       }
-      intake_.push_back(Intake{std::this_thread::get_id(), kp, cp, kn, cn, offset_chunk, size_value,
-                               inline_chunk ? ByteArray() : chunk});
-      intake_bytes_ += cn;
-      kick = intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts;
+      L.intake.push_back(Intake{std::this_thread::get_id(), kp, cp, kn, cn, offset_chunk, size_value,
+                                inline_chunk ? ByteArray() : chunk, mine});
+      L.intake_bytes += cn;
+      kick = L.intake_bytes >= kBatchBytes || L.intake.size() >= kBatchParts;
     }
-    if (kick) cv_work_.notify_one();
+    if (kick) L.cv_work.notify_one();
     Status s = Status::OK();
-    if (settle) s = settle_part(mine);
+    if (settle) s = settle_part(L, mine);
     if (stats_.on) defer_ns_.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(),
                                        std::memory_order_relaxed);
     return s;
@@ -453,16 +519,35 @@ class Pipeline {
     return ok;
   }
 
-  // An irregular part waits for its own result (the worker is asked to take
+  // The lane this client thread's part goes to (see Lane): the thread keeps
+  // its lane until it has sent it kLaneSpan bytes, and moves on only at a
+  // value's first part with bytes.
+  size_t lane_of(uint64_t offset_chunk, uint64_t cn) {
+    struct LaneOf {
+      uint64_t owner;
+      size_t lane;
+      uint64_t bytes;
+    };
+    thread_local LaneOf t = {0, 0, 0};
+    if (t.owner != id_) t = LaneOf{id_, next_lane_.fetch_add(1, std::memory_order_relaxed) % lanes_.size(), 0};
+    if (lanes_.size() > 1 && offset_chunk == 0 && cn > 0 && t.bytes >= kLaneSpan) {
+      t.lane = next_lane_.fetch_add(1, std::memory_order_relaxed) % lanes_.size();
+      t.bytes = 0;
+    }
+    t.bytes += cn;
+    return t.lane;
+  }
+
+  // An irregular part waits for its own result (its lane is asked to take
   // the intake at once) and returns PutPartValidSize's status; a refused
   // part's result is dropped here, as its order never reaches the buffer.
-  Status settle_part(uint64_t mine) {
+  Status settle_part(Lane& L, uint64_t mine) {
     settles_.fetch_add(1, std::memory_order_relaxed);
     {
       std::unique_lock<std::mutex> lk(mu_);
       if (processed_ <= mine) {
-        drain_ = true;
-        cv_work_.notify_one();
+        L.drain = true;
+        L.cv_work.notify_one();
         cv_done_.wait(lk, [&] { return processed_ > mine; });
       }
     }
@@ -470,7 +555,7 @@ class Pipeline {
     {
       std::lock_guard<std::mutex> l(res_mu_);
       const uint64_t at = mine - res_base_;   // not consumed (no order holds it yet), so still queued
-      if (at >= res_.size() || res_[at].status == 0) return Status::OK();
+      if (at >= res_.size() || !res_[at].ready || res_[at].status == 0) return Status::OK();
       r0.mode = res_[at].mode;
       cancelled_.insert((uint32_t)mine);
     }
@@ -496,40 +581,34 @@ class Pipeline {
   }
 
  private:
-  void run();
+  void run(Lane* L);
   void watch(long seconds);
   void drop_consumed();
-  void process(std::vector<Intake>& batch, uint64_t t0);
-  int gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out);
-  void host_batch(std::vector<Intake>& batch, std::vector<Result>& out);
+  void process(Lane& L, std::vector<Intake>& batch);
+  int gpu_batch(Lane& L, std::vector<Intake>& batch, std::vector<Result>& out);
+  void host_batch(Lane& L, std::vector<Intake>& batch, std::vector<Result>& out);
 
   // the 64-bit ticket of an order's 32 bits (outstanding tickets span < 2^32)
   uint64_t full_ticket(uint32_t t) const { return res_base_ + (uint32_t)(t - (uint32_t)res_base_); }
 
   const int device_;
   const uint64_t id_ = g_pipeline_ids.fetch_add(1);
-  std::thread worker_, watch_;
-  std::atomic<int> phase_{0};                // worker: 0 waiting for intake, 1 GPU batch, 2 publishing, 3 dropping
+  std::vector<std::unique_ptr<Lane>> lanes_;
+  std::atomic<size_t> next_lane_{0};
+  std::thread watch_;
   std::atomic<uint64_t> complete_waits_for_{0};   // a flush waiting for this ticket (0: none)
-  // intake (client threads, worker)
+  // tickets (client threads, lanes, flush thread)
   std::mutex mu_;
-  std::condition_variable cv_work_, cv_done_;
-  std::vector<Intake> intake_;
-  std::vector<ByteArray> intake_blocks_;   // the arena blocks intake_'s bytes live in
-  uint64_t gen_ = 0;                       // batches taken so far
-  uint64_t intake_bytes_ = 0;
-  std::chrono::steady_clock::time_point intake_since_;
+  std::condition_variable cv_done_;
   uint64_t next_ticket_ = 1;
   uint64_t processed_ = 1;           // tickets below have results
-  bool drain_ = false, stop_ = false, garbage_ = false;
-  // results (worker appends, flush thread consumes)
+  bool stop_ = false, garbage_ = false;
+  // results, by ticket (lanes fill them, in any order; the flush thread consumes)
   std::mutex res_mu_;
   std::deque<Result> res_;
   uint64_t res_base_ = 1;            // ticket of res_.front()
+  uint64_t ready_below_ = 1;         // tickets below are published
   std::unordered_set<uint32_t> cancelled_;
-  // worker only
-  std::unordered_map<std::thread::id, kdb_flush_state> state_;
-  Staging stg_;
   Inject inject_;
   // KDB_LZ4_FLUSH_MAX_PARTS=<n> -- test knob: at most n parts per GPU batch, so
   // a small stream's multipart values straddle batches (tests/test_hook_contract.py)
@@ -537,7 +616,7 @@ class Pipeline {
     const char* e = getenv("KDB_LZ4_FLUSH_MAX_PARTS");
     return e ? (size_t)strtoull(e, nullptr, 10) : (size_t)0;
   }();
-  uint64_t attempts_ = 0;
+  std::atomic<uint64_t> attempts_{0};
   Stats stats_;
   std::atomic<uint64_t> ratio_q16_{1u << 16};
   std::atomic<uint64_t> defer_ns_{0};           // client threads' time in defer() (stats only)
@@ -547,69 +626,66 @@ class Pipeline {
   std::atomic<uint64_t> stall_ns_{0}, stalls_{0}, stall_max_ns_{0}, stall_max_at_ns_{0};   // client gaps > 1 ms between puts   // accounted / raw bytes of the last batch, x 2^16
 };
 
-void Pipeline::run() {
+void Pipeline::run(Lane* Lp) {
+  Lane& L = *Lp;
   const Clock::time_point t_init = Clock::now();
-  kdb_lz4_set_device(device_);
+  kdb_lz4_set_device(L.device);
   (void)kdb_lz4_warmup();   // this device's first launches, once per device
-  StagingPool::get().take(device_, stg_);
+  StagingPool::get().take(L.device, L.stg);
   // the first batch's staging (pinned host + device) is allocated here, while
   // the database opens, not under the first puts: until a batch completes,
   // deferred chunks are accounted at their raw size (LZ4FlushAccount), and a
   // slow first batch had let 1 M 100-byte puts fill the write buffer on that
   // prior and block on its flush (client_embedded)
-  if (!stg_.host) (void)stg_.reserve(16ull << 20, 16ull << 20);
-  if (stats_.on) stats_.init_ms = ms_since(t_init);
+  if (!L.stg.host) (void)L.stg.reserve(16ull << 20, 16ull << 20);
+  L.init_ms = ms_since(t_init);
   std::vector<Intake> batch;
   std::vector<ByteArray> blocks;
   for (;;) {
-    uint64_t t0;
     {
       std::unique_lock<std::mutex> lk(mu_);
       for (;;) {
-        if (garbage_) {
+        if (L.index == 0 && garbage_) {   // (lane 0 frees the consumed results)
           garbage_ = false;
           lk.unlock();
-          phase_.store(3, std::memory_order_relaxed);
+          L.phase.store(3, std::memory_order_relaxed);
           drop_consumed();
-          phase_.store(0, std::memory_order_relaxed);
+          L.phase.store(0, std::memory_order_relaxed);
           lk.lock();
           continue;
         }
-        if (intake_.empty()) {
-          if (drain_) {
-            drain_ = false;
-            cv_done_.notify_all();
-          }
+        if (L.intake.empty()) {
+          L.drain = false;
           if (stop_) {
-            StagingPool::get().put(device_, stg_);
+            StagingPool::get().put(L.device, L.stg);
             return;
           }
-          cv_work_.wait(lk);
+          L.cv_work.wait(lk);
           continue;
         }
-        if (stop_ || drain_ || intake_bytes_ >= kBatchBytes || intake_.size() >= kBatchParts ||
-            std::chrono::steady_clock::now() - intake_since_ >= kBatchAge)
+        if (stop_ || L.drain || L.intake_bytes >= kBatchBytes || L.intake.size() >= kBatchParts ||
+            Clock::now() - L.intake_since >= kBatchAge)
           break;
-        cv_work_.wait_until(lk, intake_since_ + kBatchAge);
+        L.cv_work.wait_until(lk, L.intake_since + kBatchAge);
       }
-      if (max_parts_ && intake_.size() > max_parts_) {   // (test knob: the rest stays queued)
-        batch.assign(std::make_move_iterator(intake_.begin()), std::make_move_iterator(intake_.begin() + (long)max_parts_));
-        intake_.erase(intake_.begin(), intake_.begin() + (long)max_parts_);
-        blocks = intake_blocks_;                           // (the rest's arena blocks stay registered too)
-        intake_bytes_ = 0;
-        for (const Intake& e : intake_) intake_bytes_ += e.cn;
-        intake_since_ = std::chrono::steady_clock::now();
+      if (max_parts_ && L.intake.size() > max_parts_) {   // (test knob: the rest stays queued)
+        batch.assign(std::make_move_iterator(L.intake.begin()),
+                     std::make_move_iterator(L.intake.begin() + (long)max_parts_));
+        L.intake.erase(L.intake.begin(), L.intake.begin() + (long)max_parts_);
+        blocks = L.intake_blocks;                          // (the rest's arena blocks stay registered too)
+        L.intake_bytes = 0;
+        for (const Intake& e : L.intake) L.intake_bytes += e.cn;
+        L.intake_since = Clock::now();
       } else {
-        batch.swap(intake_);
-        blocks.swap(intake_blocks_);
-        intake_bytes_ = 0;
+        batch.swap(L.intake);
+        blocks.swap(L.intake_blocks);
+        L.intake_bytes = 0;
       }
-      gen_++;
-      t0 = processed_;
+      L.gen++;
     }
-    phase_.store(1, std::memory_order_relaxed);
-    process(batch, t0);   // publishes the results, then processed_
-    phase_.store(0, std::memory_order_relaxed);
+    L.phase.store(1, std::memory_order_relaxed);
+    process(L, batch);   // publishes the results, then processed_
+    L.phase.store(0, std::memory_order_relaxed);
     batch.clear();
     blocks.clear();
   }
@@ -620,36 +696,49 @@ void Pipeline::watch(long seconds) {
   while (!stop_) {
     const auto until = std::chrono::steady_clock::now() + std::chrono::seconds(seconds);
     if (cv_done_.wait_until(lk, until, [&] { return stop_; })) break;
-    fprintf(stderr,
-            "lz4_flush_watch pipeline %llu tickets_issued %llu processed_below %llu intake %zu blocks %zu drain %d "
-            "host_batches %llu worker_phase %d flush_waits_for %llu batches %llu\n",
+    fprintf(stderr, "lz4_flush_watch pipeline %llu tickets_issued %llu processed_below %llu host_batches %llu "
+            "flush_waits_for %llu batches %llu",
             (unsigned long long)id_, (unsigned long long)next_ticket_, (unsigned long long)processed_,
-            intake_.size(), intake_blocks_.size(), (int)drain_, (unsigned long long)host_batches_.load(),
-            phase_.load(), (unsigned long long)complete_waits_for_.load(), (unsigned long long)gpu_batches_.load());
+            (unsigned long long)host_batches_.load(), (unsigned long long)complete_waits_for_.load(),
+            (unsigned long long)gpu_batches_.load());
+    for (auto& L : lanes_)
+      fprintf(stderr, " | lane %zu device %d intake %zu blocks %zu drain %d phase %d", L->index, L->device,
+              L->intake.size(), L->intake_blocks.size(), (int)L->drain, L->phase.load());
+    fprintf(stderr, "\n");
   }
 }
 
-void Pipeline::process(std::vector<Intake>& batch, uint64_t t0) {
+void Pipeline::process(Lane& L, std::vector<Intake>& batch) {
   std::vector<Result> out(batch.size());
-  int rc = gpu_batch(batch, out);
+  int rc = gpu_batch(L, batch, out);
   if (rc != KDB_LZ4_OK) {   // once more, on a fresh stream and fresh staging
     log::emerg("LZ4FlushPipeline", "GPU batch of %zu parts failed (%d); retrying", batch.size(), rc);
-    stg_.drop();
-    rc = gpu_batch(batch, out);
+    L.stg.drop();
+    rc = gpu_batch(L, batch, out);
   }
   if (rc != KDB_LZ4_OK) {
     log::emerg("LZ4FlushPipeline", "GPU batch failed twice (%d): %zu parts stored uncompressed", rc, batch.size());
-    stg_.drop();
+    L.stg.drop();
     for (Result& r : out) r = Result();
-    host_batch(batch, out);
+    host_batch(L, batch, out);
   }
+  // publish by ticket (lanes finish in any order); processed_ is the lowest
+  // ticket any lane still holds
+  uint64_t w;
   {
     std::lock_guard<std::mutex> l(res_mu_);
-    for (Result& r : out) res_.push_back(std::move(r));
+    for (size_t i = 0; i < batch.size(); i++) {
+      const uint64_t at = batch[i].ticket - res_base_;
+      if (at >= res_.size()) res_.resize(at + 1);
+      res_[at] = std::move(out[i]);
+      res_[at].ready = true;
+    }
+    while (ready_below_ - res_base_ < res_.size() && res_[ready_below_ - res_base_].ready) ready_below_++;
+    w = ready_below_;
   }
   {
     std::lock_guard<std::mutex> l(mu_);
-    processed_ = t0 + batch.size();
+    if (w > processed_) processed_ = w;
   }
   cv_done_.notify_all();
 }
@@ -664,7 +753,7 @@ void Pipeline::process(std::vector<Intake>& batch, uint64_t t0) {
 // 173-180, 213-245); each thread's carried state is the reference's after the
 // same calls, so a later GPU batch continues from it.  No LZ4 on the host;
 // the CRC32C is the drop-in's host Crc32cExtend (compressor.cc).
-void Pipeline::host_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
+void Pipeline::host_batch(Lane& L, std::vector<Intake>& batch, std::vector<Result>& out) {
   const uint32_t m = (uint32_t)batch.size();
   uint64_t dis_bytes = 0;
   for (const Intake& e : batch) dis_bytes += e.cn + 8;
@@ -674,7 +763,7 @@ void Pipeline::host_batch(std::vector<Intake>& batch, std::vector<Result>& out) 
   for (uint32_t i = 0; i < m; i++) {
     const Intake& e = batch[i];
     Result& r = out[i];
-    kdb_flush_state& S = state_[e.tid];
+    kdb_flush_state& S = L.state[e.tid];
     const uint64_t csz = e.cn, off = e.offset_chunk, V = e.size_value;
     const uint64_t pad = (V / 65536u + 1u) * 8u;                     // format.h:63-71
     const bool first = off == 0, last = csz + off == V, do_comp = csz != 0;
@@ -717,10 +806,9 @@ void Pipeline::host_batch(std::vector<Intake>& batch, std::vector<Result>& out) 
 
 // The batch through the GPU: layout (segments, runs), staging, one
 // kdb_flush_parts_batch, results.  0 or a KDB_LZ4_E* code.
-int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
+int Pipeline::gpu_batch(Lane& L, std::vector<Intake>& batch, std::vector<Result>& out) {
   const Clock::time_point t_start = Clock::now();
-  ++attempts_;
-  if (inject_.fails(attempts_)) return KDB_LZ4_EHIP;
+  if (inject_.fails(attempts_.fetch_add(1) + 1)) return KDB_LZ4_EHIP;
   const uint32_t m = (uint32_t)batch.size();
   // ---- layout: a segment is one thread's consecutive parts of one value; a
   // run is one thread's segments whose policy state chains (a new run starts
@@ -745,8 +833,8 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
       run_tid.push_back(e.tid);
       kdb_flush_state s{};
       if (!seen) {
-        auto st = state_.find(e.tid);
-        if (st != state_.end()) s = st->second;
+        auto st = L.state.find(e.tid);
+        if (st != L.state.end()) s = st->second;
       }
       carry.push_back(s);
       const uint32_t sg = (uint32_t)seg_run.size();
@@ -813,9 +901,9 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
                  p_total = p_carry + a256(sizeof(kdb_flush_state) * nruns), out_bytes = p_total + 256;
   const uint64_t d_frames = d_out + out_bytes, dev_bytes = d_frames + a256(frame_cap);
   const uint64_t h_out = in_bytes, h_frames = h_out + out_bytes, host_bytes = h_frames + a256(frame_cap);
-  if (!stg_.reserve(host_bytes, dev_bytes)) return KDB_LZ4_EHIP;
-  char* hb = static_cast<char*>(stg_.host);
-  char* db = static_cast<char*>(stg_.dev);
+  if (!L.stg.reserve(host_bytes, dev_bytes)) return KDB_LZ4_EHIP;
+  char* hb = static_cast<char*>(L.stg.host);
+  char* db = static_cast<char*>(L.stg.dev);
   auto H64 = [&](uint64_t o) { return reinterpret_cast<uint64_t*>(hb + o); };
   auto H32 = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(hb + o); };
   {
@@ -843,7 +931,7 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
   }
   const double t_stage = ms_since(t_start);
   const Clock::time_point t_gpu = Clock::now();
-  void* st = stg_.stream;
+  void* st = L.stg.stream;
   auto D8 = [&](uint64_t o) { return reinterpret_cast<uint8_t*>(db + o); };
   auto D32 = [&](uint64_t o) { return reinterpret_cast<uint32_t*>(db + o); };
   auto D64 = [&](uint64_t o) { return reinterpret_cast<uint64_t*>(db + o); };
@@ -904,21 +992,21 @@ int Pipeline::gpu_batch(std::vector<Intake>& batch, std::vector<Result>& out) {
     }
   }
   // each thread's state after its last run of the batch
-  for (uint32_t r = 0; r < nruns; r++) state_[run_tid[r]] = cout[r];
+  for (uint32_t r = 0; r < nruns; r++) L.state[run_tid[r]] = cout[r];
   {  // what the batch's chunks take in the buffer once final, per raw byte
     uint64_t acc = 0;
     for (uint32_t q = 0; q < m; q++)
       acc += parts[q].status == 0 && parts[q].mode != KDB_FLUSH_RAW ? parts[q].size : batch[perm[q]].cn;
     if (raw_bytes) ratio_q16_.store(std::min<uint64_t>((acc << 16) / raw_bytes, 1u << 17), std::memory_order_relaxed);
   }
-  if (stats_.on && stats_.batches == 0) stats_.first_batch_ms = ms_since(t_start);
-  stats_.batches++;
+  if (L.batches == 0) L.first_batch_ms = ms_since(t_start);
+  L.batches++;
   gpu_batches_.fetch_add(1, std::memory_order_relaxed);   // (read by watch(), which holds mu_ only)
-  stats_.parts += m;
-  stats_.raw_bytes += raw_bytes;
-  stats_.stage_ms += t_stage;
-  stats_.gpu_ms += t_gpu_ms;
-  stats_.results_ms += ms_since(t_res);
+  L.parts += m;
+  L.raw_bytes += raw_bytes;
+  L.stage_ms += t_stage;
+  L.gpu_ms += t_gpu_ms;
+  L.results_ms += ms_since(t_res);
   return KDB_LZ4_OK;
 }
 
@@ -941,8 +1029,10 @@ void Pipeline::complete(std::vector<Order>& orders) {
     std::unique_lock<std::mutex> lk(mu_);
     if (processed_ <= newest) {
       const Clock::time_point tw = Clock::now();
-      drain_ = true;
-      cv_work_.notify_one();
+      for (auto& L : lanes_) {
+        L->drain = true;
+        L->cv_work.notify_one();
+      }
       complete_waits_for_.store(newest, std::memory_order_relaxed);
       cv_done_.wait(lk, [&] { return processed_ > newest; });
       complete_waits_for_.store(0, std::memory_order_relaxed);
@@ -998,16 +1088,17 @@ void Pipeline::complete(std::vector<Order>& orders) {
   if (stats_.on && stats_.passes.size() < 64)
     stats_.passes.push_back({std::chrono::duration<double, std::milli>(t0 - stats_.born).count(), c, orders.size(),
                              !orders.empty() && orders[0].write_options.sync});
-  // the consumed results are dropped by the worker (drop_consumed), off this thread
+  // the consumed results are dropped by lane 0's worker (drop_consumed), off this thread
   {
     std::lock_guard<std::mutex> l2(mu_);
     garbage_ = true;
   }
-  cv_work_.notify_one();
+  lanes_[0]->cv_work.notify_one();
 }
 
-// Worker: drops the consumed (or cancelled) results at the front, freeing
-// their buffers here rather than on the flush thread.
+// Lane 0's worker: drops the consumed (or cancelled) results at the front,
+// freeing their buffers here rather than on the flush thread.  A cancelled
+// ticket a lane has not published yet stays (its slot is still to be filled).
 void Pipeline::drop_consumed() {
   std::deque<Result> dead;
   {
@@ -1016,7 +1107,7 @@ void Pipeline::drop_consumed() {
     while (k < res_.size()) {
       const uint32_t t = (uint32_t)(res_base_ + k);
       auto c = cancelled_.find(t);
-      if (!res_[k].consumed && c == cancelled_.end()) break;
+      if (!res_[k].ready || (!res_[k].consumed && c == cancelled_.end())) break;
       if (c != cancelled_.end()) cancelled_.erase(c);
       k++;
     }

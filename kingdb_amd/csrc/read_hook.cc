@@ -11,6 +11,8 @@
 // ends in frames.  kdb_get_values_batch's verify mode 2 is exactly that check.
 #include "interface/lz4_read.h"
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -99,16 +101,19 @@ struct ReadStats {
     if (on)
       fprintf(stderr,
               "lz4_read_stats batches %llu values %llu stored_bytes %llu gets %llu peek_ms %.2f stage_ms %.2f "
-              "gpu_ms %.2f arena_ms %.2f join_ms %.2f sync_batches %llu sync_ms %.2f\n",
+              "gpu_ms %.2f arena_ms %.2f join_ms %.2f sync_batches %llu sync_ms %.2f devices_mask %llx\n",
               (unsigned long long)batches, (unsigned long long)values, (unsigned long long)stored,
               (unsigned long long)gets, peek_ms, stage_ms, gpu_ms, arena_ms, join_ms,
-              (unsigned long long)sync_batches, sync_ms);
+              (unsigned long long)sync_batches, sync_ms, (unsigned long long)devices_mask());
   }
+  static unsigned long long devices_mask();
   void add(double& x, double ms) {
     std::lock_guard<std::mutex> l(mu);
     x += ms;
   }
 };
+std::atomic<uint64_t> g_read_devices_used{0};   // bit d: a read-ahead batch ran on device d (stats)
+unsigned long long ReadStats::devices_mask() { return g_read_devices_used.load(); }
 ReadStats g_read_stats;
 using Clock = std::chrono::steady_clock;
 inline double ms_since(Clock::time_point t0) {
@@ -246,16 +251,19 @@ namespace {
 struct StagingPool {
   std::mutex mu;
   std::vector<ReadStaging*> free;
-  ReadStaging* take() {
+  ReadStaging* take(int device) {   // one already bound to `device`, if any
     std::lock_guard<std::mutex> l(mu);
-    if (free.empty()) return new ReadStaging();
-    ReadStaging* s = free.back();
-    free.pop_back();
-    return s;
+    for (size_t i = free.size(); i-- > 0;)
+      if (free[i]->device == device) {
+        ReadStaging* s = free[i];
+        free.erase(free.begin() + (long)i);
+        return s;
+      }
+    return new ReadStaging();
   }
   void give(ReadStaging* s) {
     std::lock_guard<std::mutex> l(mu);
-    if (free.size() < 4) {
+    if (free.size() < 16) {
       free.push_back(s);
       return;
     }
@@ -263,6 +271,23 @@ struct StagingPool {
   }
 };
 StagingPool g_read_pool;
+
+// The device a read-ahead batch decodes on: the batches of every iterator
+// take the visible devices in turn, starting from the asking thread's
+// (KDB_LZ4_READ_DEVICES=<n> caps how many); the batches are independent.
+int read_device(int base) {
+  static const int count = [] {
+    int c = 1;
+    return kdb_lz4_device_count(&c) == KDB_LZ4_OK && c > 0 ? c : 1;
+  }();
+  static const int n = [] {
+    const char* e = getenv("KDB_LZ4_READ_DEVICES");
+    const long want = e && *e ? atol(e) : count;
+    return (int)std::max(1L, std::min<long>(count, want));
+  }();
+  static std::atomic<unsigned> next{0};
+  return n > 1 ? (base + (int)(next.fetch_add(1, std::memory_order_relaxed) % (unsigned)n)) % count : base;
+}
 
 // The entries a plan names, headers decoded as Next() decodes them
 // (EntryHeader::DecodeFrom, storage/format.h); *resume: where the next plan
@@ -346,7 +371,8 @@ struct LZ4ReadAhead::Batch {
     if (recs.empty()) return;
     std::vector<uint64_t> at, len;
     std::vector<int32_t> st;
-    ReadStaging* stg = g_read_pool.take();
+    ReadStaging* stg = g_read_pool.take(device);
+    if (device >= 0 && device < 64) g_read_devices_used.fetch_or(1ull << device, std::memory_order_relaxed);
     const int rc = gpu_decode(*stg, recs.data(), (uint32_t)recs.size(), plan.read_options.verify_checksums, &arena,
                               &at, &len, &st);
     if (rc != KDB_LZ4_OK) {
@@ -388,6 +414,7 @@ void LZ4ReadAhead::start_next(const Peek& peek, uint64_t max_size) {
   if (!plan.base) return;
   int device = 0;
   if (kdb_lz4_get_device(&device) != KDB_LZ4_OK) return;
+  device = read_device(device);
   next_ = new Batch();
   Batch* b = next_;
   b->th = std::thread([b, max_size, device](LZ4PeekPlan pl) { b->build(pl, nullptr, max_size, device); },

@@ -278,17 +278,16 @@ fail:
 
 /* ---- CRC32C (Castagnoli, reflected 0x82F63B78): crc32c.cc:296-340 ------- */
 static uint32_t crc_table[256];
-static int crc_init_done = 0;
 static void crc_init(void) {
   for (uint32_t i = 0; i < 256; i++) {
     uint32_t c = i;
     for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
     crc_table[i] = c;
   }
-  crc_init_done = 1;
 }
+/* filled before main (callers may be concurrent threads) */
+__attribute__((constructor)) static void crc_init_ctor(void) { crc_init(); }
 uint32_t orc_crc32c_extend(uint32_t crc, const uint8_t* p, size_t n) {
-  if (!crc_init_done) crc_init();
   uint32_t l = crc ^ 0xffffffffu;
   for (size_t i = 0; i < n; i++) l = crc_table[(l ^ p[i]) & 0xff] ^ (l >> 8);
   return l ^ 0xffffffffu;
@@ -373,16 +372,14 @@ int orc_frame_uncompress(const uint8_t* frame, uint8_t* out, uint64_t* out_n, ui
 /* crc32c::crc8 (crc32c.cc:439-475): reflected CRC-8, table for polynomial 0xB2
  * (reflected), pre/post xor 0xff; crc8(c, p, 0) returns c unchanged. */
 static uint8_t crc8_table[256];
-static int crc8_done = 0;
-uint8_t orc_crc8(unsigned crc, const uint8_t* p, size_t n) {
-  if (!crc8_done) {
-    for (unsigned i = 0; i < 256; i++) {
-      unsigned c = i;
-      for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xB2u : c >> 1;
-      crc8_table[i] = (uint8_t)c;
-    }
-    crc8_done = 1;
+__attribute__((constructor)) static void crc8_init(void) {   /* before main: callers may be concurrent */
+  for (unsigned i = 0; i < 256; i++) {
+    unsigned c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xB2u : c >> 1;
+    crc8_table[i] = (uint8_t)c;
   }
+}
+uint8_t orc_crc8(unsigned crc, const uint8_t* p, size_t n) {
   if (n == 0) return (uint8_t)crc;
   crc ^= 0xffu;
   for (size_t i = 0; i < n; i++) crc = crc8_table[(crc ^ p[i]) & 0xffu];

@@ -87,19 +87,31 @@ needs_ref = pytest.mark.skipif(not os.path.isdir("/root/reference"),
 
 
 @needs_ref
-def test_kingdb_hook_threads_tsan(tmp_path):
+@pytest.mark.parametrize("devices", [1, 4])
+def test_kingdb_hook_threads_tsan(tmp_path, devices):
     """4 client threads writing single-part and multipart values through the
     flush hook, then 4 readers (Get, MultipartReader) and an iteration through
-    the read hooks; no race in our code."""
+    the read hooks; no race in our code.  With 4 modelled devices the flush
+    pipeline runs one lane (worker, staging, stream) per device and the
+    read-ahead spreads its batches over them: every batch ran on the device
+    its stream belongs to (the model refuses any other), all four devices
+    took batches, and every value reads back."""
     _make(["-C", ORACLE, "kingdb_san", "SAN=thread"])
     # small read-ahead batches, so the iteration runs its helper threads too
-    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=0 history_size=4", KDB_LZ4_READ_BATCH="32")
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=0 history_size=4", KDB_LZ4_READ_BATCH="32",
+               KDB_LZ4_CPU_MODEL_DEVICES=str(devices), KDB_LZ4_CPU_MODEL_STATS="1", KDB_LZ4_FLUSH_STATS="1")
     r = subprocess.run([os.path.join(ORACLE, "_ref", "kingdb_tsan", "hook_mt"), str(tmp_path / "db"), "4", "60"],
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     assert r.stdout.startswith("ok:"), r.stdout
     ours = _our_races(r.stderr)
     assert not ours, "\n\n".join(ours[:3])
+    per_dev = re.search(r"cpu_model_batches(( device\d+ \d+)+)", r.stderr)
+    assert per_dev, r.stderr[-2000:]
+    counts = [int(x) for x in re.findall(r"device\d+ (\d+)", per_dev.group(1))]
+    assert len(counts) == devices and all(c > 0 for c in counts), per_dev.group(0)
+    lanes = [ln for ln in r.stderr.splitlines() if ln.startswith("lz4_flush_lanes")]
+    assert lanes and lanes[0].startswith(f"lz4_flush_lanes {devices}"), lanes
 
 
 @needs_ref

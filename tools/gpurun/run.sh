@@ -54,7 +54,7 @@ for s in "$@"; do
   say "$s"
   case $s in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "${O}_tests.log" 2>&1 || fail tests $? "${O}_tests.log"
+      timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu --durations=25 --timeout 300 --timeout-method thread > "${O}_tests.log" 2>&1 || fail tests $? "${O}_tests.log"
       tail -2 "${O}_tests.log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "${O}_smoke.log" 2>&1 || fail smoke $? "${O}_smoke.log"
