@@ -53,6 +53,11 @@ int kdb_lz4_selftest(int device, int* state, uint32_t* bad_lanes);
  * object is loaded and the runtime's first-launch costs are paid here, not
  * inside a caller's timed or latency-critical path).  Synchronous; idempotent. */
 int kdb_lz4_warmup(void);
+/* The per-call decode path's resident service (kingdb_amd/csrc/service.h) on
+ * `device`: *launches = instances launched so far, *served = requests the
+ * instances that exited served, *alive = 1 while one is resident.  All 0 when
+ * the service was never used on the device.  No HIP call. */
+int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint32_t* alive);
 /* The kernels (rocprof names, ';'-separated) that the calling thread's last
  * compress or decompress batch queued.  No HIP call. */
 int kdb_lz4_last_kernels(char* buf, uint64_t cap);

@@ -6,13 +6,18 @@
 // (pinned host + device buffers + a private stream) that grows on demand.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/kdb_lz4.h"
 #include "lz4_device.h"
+#include "service.h"
 
 namespace kdb_lz4 {
 hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
@@ -25,6 +30,7 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* target, uint32_t* out_len, int32_t* ret);
 hipError_t launch_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed,
                          hipStream_t st);
+hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
 }  // namespace kdb_lz4
 
 using namespace kdb_lz4;
@@ -133,11 +139,181 @@ inline Meta read_meta(const uint8_t* p) {
   return m;
 }
 
+// ---- the resident decode service (service.h), one per device and process.
+// KDB_LZ4_SERVICE=0 turns it off (every call launches, as before);
+// KDB_LZ4_SERVICE_IDLE_US (default 2000) is how long the wave waits for the
+// next request before it exits.
+bool service_on() {
+  static const bool on = [] {
+    const char* e = getenv("KDB_LZ4_SERVICE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
+struct Service {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  SvcBox* box = nullptr;     // host view (pinned, coherent, mapped)
+  SvcBox* dbox = nullptr;    // its device address
+  uint64_t idle_ticks = 0, life_ticks = 0;
+  std::vector<int> free_slots;
+  bool ok = false;
+  int device = 0;
+  bool launch() {            // (mu held) a new instance, behind any old one on the stream
+    __atomic_store_n(&box->alive, 1u, __ATOMIC_SEQ_CST);
+    if (launch_decode_service(stream, dbox, idle_ticks, life_ticks) != hipSuccess) {
+      __atomic_store_n(&box->alive, 0u, __ATOMIC_SEQ_CST);
+      return false;
+    }
+    box->launches++;
+    return true;
+  }
+  void ensure_running() {
+    if (__atomic_load_n(&box->alive, __ATOMIC_SEQ_CST) != 0u) return;
+    std::lock_guard<std::mutex> l(mu);
+    if (__atomic_load_n(&box->alive, __ATOMIC_SEQ_CST) == 0u) (void)launch();
+  }
+};
+
+std::mutex g_svc_mu;
+std::vector<Service*>& services() {
+  static std::vector<Service*>* v = new std::vector<Service*>();   // never destroyed: waves may still read them
+  return *v;
+}
+// process teardown: every service wave is told to leave, and is given a
+// moment to (it also leaves by itself once idle)
+void stop_services() {
+  std::lock_guard<std::mutex> l(g_svc_mu);
+  for (Service* s : services()) {
+    if (!s || !s->ok) continue;
+    __atomic_store_n(&s->box->stop, 1u, __ATOMIC_SEQ_CST);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&s->box->alive, __ATOMIC_SEQ_CST) != 0u &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50)) {
+    }
+  }
+}
+
+Service* service_of(int dev) {
+  std::lock_guard<std::mutex> l(g_svc_mu);
+  std::vector<Service*>& v = services();
+  if ((int)v.size() <= dev) v.resize(dev + 1, nullptr);
+  if (v[dev]) return v[dev]->ok ? v[dev] : nullptr;
+  Service* s = new Service();
+  v[dev] = s;
+  s->device = dev;
+  void* h = nullptr;
+  int rate_khz = 0;
+  if (hipHostMalloc(&h, sizeof(SvcBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+  memset(h, 0, sizeof(SvcBox));
+  s->box = static_cast<SvcBox*>(h);
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&s->dbox), h, 0) != hipSuccess ||
+      hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0)
+    return nullptr;
+  const char* e = getenv("KDB_LZ4_SERVICE_IDLE_US");
+  const uint64_t idle_us = e && *e ? strtoull(e, nullptr, 10) : 2000u;
+  s->idle_ticks = idle_us * (uint64_t)rate_khz / 1000u;
+  s->life_ticks = 500ull * (uint64_t)rate_khz;   // 500 ms, then a fresh instance
+  for (int i = (int)kSvcSlots - 1; i >= 0; i--) s->free_slots.push_back(i);
+  static bool registered = false;
+  if (!registered) {
+    registered = true;
+    atexit(stop_services);
+  }
+  s->ok = true;
+  return s;
+}
+
+// A calling thread's slot in a device's mailbox, returned when the thread
+// exits; -1 when all 64 are taken (the call launches instead).
+struct SlotLease {
+  std::unordered_map<int, int> slot;   // device -> slot (-1: none)
+  ~SlotLease() {
+    for (auto& kv : slot) {
+      Service* s = services().size() > (size_t)kv.first ? services()[kv.first] : nullptr;
+      if (!s || kv.second < 0) continue;
+      std::lock_guard<std::mutex> l(s->mu);
+      s->free_slots.push_back(kv.second);
+    }
+  }
+};
+thread_local SlotLease t_lease;
+int slot_of(Service* s) {
+  SlotLease& lease = t_lease;
+  auto it = lease.slot.find(s->device);
+  if (it != lease.slot.end()) return it->second;
+  int k = -1;
+  {
+    std::lock_guard<std::mutex> l(s->mu);
+    if (!s->free_slots.empty()) {
+      k = s->free_slots.back();
+      s->free_slots.pop_back();
+    }
+  }
+  lease.slot[s->device] = k;
+  return k;
+}
+
+// One LZ4_decompress_safe_partial through the service; false when it could
+// not be used (no service, no free slot, no answer within a second -- the
+// caller then launches as before).  *ret = the kernel's return word.
+bool service_decode(const char* source, char* dest, uint32_t C, uint32_t O, int target, int* ret) {
+  if (!service_on()) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  Service* s = service_of(dev);
+  if (!s) return false;
+  const int k = slot_of(s);
+  if (k < 0) return false;
+  SvcSlot& sl = s->box->slot[k];
+  sl.csize = C;
+  sl.osize = O;
+  sl.target = (uint32_t)target;
+  if (C) memcpy(sl.in, source, C);
+  const uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
+  __atomic_store_n(&s->box->req[k], want, __ATOMIC_RELEASE);     // the doorbell, after the arguments
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);                        // ... and before alive is read
+  s->ensure_running();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spins = 1;; spins++) {
+    if (__atomic_load_n(&s->box->done[k], __ATOMIC_ACQUIRE) == want) break;
+    __builtin_ia32_pause();
+    if ((spins & 1023u) == 0) {
+      const auto waited = std::chrono::steady_clock::now() - t0;
+      if (waited > std::chrono::microseconds(200)) s->ensure_running();   // it had just left: once more
+      if (waited > std::chrono::seconds(1)) {
+        // no answer (the device busy past a second?): this thread gives the
+        // slot up for good (the wave may still write it) and launches
+        t_lease.slot[s->device] = -1;
+        return false;
+      }
+    }
+  }
+  *ret = __atomic_load_n(&sl.ret, __ATOMIC_ACQUIRE);
+  if (*ret > 0) memcpy(dest, sl.out, (size_t)*ret);
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
 
 int kdb_lz4_version(void) { return 10000; }
+
+int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint32_t* alive) {
+  if (!launches || !served || !alive || device < 0) return KDB_LZ4_EINVAL;
+  *launches = *served = *alive = 0;
+  std::lock_guard<std::mutex> l(g_svc_mu);
+  const std::vector<Service*>& v = services();
+  const Service* s = (size_t)device < v.size() ? v[device] : nullptr;
+  if (!s || !s->ok) return KDB_LZ4_OK;
+  *launches = __atomic_load_n(&s->box->launches, __ATOMIC_ACQUIRE);
+  *served = __atomic_load_n(&s->box->served, __ATOMIC_ACQUIRE);
+  *alive = __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE);
+  return KDB_LZ4_OK;
+}
 
 int kdb_lz4_device_count(int* count) {
   if (!count) return KDB_LZ4_EINVAL;
@@ -358,6 +534,10 @@ int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compress
   // the LDS-resident decoder's share (lz4_decompress.hip: output <= its split,
   // block <= that output's bound + a frame header)
   const bool zc = O <= kZeroCopyMax && C <= kZeroCopyMax + kZeroCopyMax / 255u + 24u;
+  if (zc && C <= kSvcMaxIn && O <= kSvcMaxOut) {   // the resident decode service (service.h)
+    int sret = 0;
+    if (service_decode(source, dest, C, O, targetOutputSize, &sret)) return sret == KDB_LZ4_VALUE_UNSUPPORTED ? -1 : sret;
+  }
   if (zc) {                                      // zero-copy: [meta][in][out] in mapped host memory
     const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)C + 16);
     if (c.reserve(out_at + align16((size_t)O + 16), 0) != KDB_LZ4_OK) return -1;

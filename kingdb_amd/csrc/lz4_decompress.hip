@@ -25,6 +25,7 @@
 #include <string>
 
 #include "lz4_device.h"
+#include "service.h"
 
 namespace kdb_lz4 {
 
@@ -929,6 +930,86 @@ __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
                             out_len, ret, work_small, batch_small, 1u, nq);
 }
 
+// ---------------------------------------------------------------------------
+// The resident decode service (service.h): one wave that serves per-call
+// LZ4_decompress_safe_partial requests (lz4.cc:1050-1053, blocks whose output
+// fits kSvcMaxOut) from a mailbox in pinned host memory, with the same
+// staging and decode_block as small_decode_loop above.  Every wave reaches an
+// exit: after idle_ticks of no requests, after life_ticks in all, or at the
+// host's stop.  Host memory is read and written with system-scope atomics
+// (doorbells, arguments, results) or plain vector loads/stores ordered by them.
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t sys_peek(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v, int order) {
+  if (order == __ATOMIC_RELEASE) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  else __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t lane = lane_id();
+  constexpr uint32_t s_in_cap = (kSvcMaxIn + 32u + 15u) & ~15u;   // small_decode_loop's layout
+  uint8_t* s_in = smem;
+  uint8_t* s_out = smem + s_in_cap;
+  uint32_t seen = sys_load(&box->done[lane]);   // lane i: the last request of slot i served
+  const uint64_t t0 = wall_clock64();
+  uint64_t t_last = t0;
+  uint32_t served = 0;
+#pragma unroll 1
+  for (;;) {
+    const uint32_t r = sys_load(&box->req[lane]);   // the 64 doorbells: one 256-byte read
+    uint64_t pend = ballot(r != seen);
+    if (pend == 0) {
+      const uint64_t now = wall_clock64();
+      const bool stop = sys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
+      if (stop || old || now - t_last > idle_ticks) {
+        // leave: clear alive, then look at the doorbells once more (a caller
+        // that rang before it read alive is served here)
+        if (lane == 0) sys_store(&box->alive, 0u, __ATOMIC_SEQ_CST);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        const uint32_t r2 = sys_load(&box->req[lane]);
+        if (stop || old || ballot(r2 != seen) == 0) break;
+        if (lane == 0) sys_store(&box->alive, 1u, __ATOMIC_SEQ_CST);
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(4);
+      continue;
+    }
+#pragma unroll 1
+    while (pend) {
+      const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1u;
+      const uint32_t want = readlane(r, sidx);
+      SvcSlot* sl = &box->slot[sidx];
+      const int csize = (int)uni(sys_peek(&sl->csize)), osize = (int)uni(sys_peek(&sl->osize));
+      const int tgt = (int)uni(sys_peek(&sl->target));
+      int rc = (int)kUnsupported;
+      if (csize >= 0 && osize >= 0 && (uint32_t)csize <= kSvcMaxIn && (uint32_t)osize <= kSvcMaxOut) {
+        const uint32_t head = stage_to_lds(sl->in, (uint32_t)csize, s_in);
+        if (lane < 16u) s_in[head + (uint32_t)csize + lane] = 0;   // OOB bytes read as 0
+        __syncthreads();
+        rc = decode_block(s_in, head, csize, s_out, osize, tgt);
+        if (rc > 0) flush_lds_to_global(sl->out, s_out, 0, (uint32_t)rc);
+        __syncthreads();
+      }
+      if (lane == 0) {
+        sys_store(reinterpret_cast<uint32_t*>(&sl->ret), (uint32_t)rc, __ATOMIC_RELEASE);
+        sys_store(&box->done[sidx], want, __ATOMIC_RELEASE);   // after the bytes and ret
+      }
+      if (lane == sidx) seen = want;
+      served++;
+    }
+    t_last = wall_clock64();
+  }
+  if (lane == 0) sys_store(&box->served, sys_peek(&box->served) + served, __ATOMIC_RELEASE);
+}
+
+hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
+
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
   // staged block (16 B alignment head + block + 16 zero bytes) | output window
   // + 64 B slack; the register window reaches 256 B past the block
@@ -1035,6 +1116,12 @@ constexpr uint32_t kOutSmallMax = k64KLimit - 1u;
 // the LDS decoder's limit inside lz4_decompress_mixed_kernel: its staged block
 // and window (decompress_lds_bytes) fit the ring decoder's LDS
 constexpr uint32_t kMixedOutSmall = 6144u;
+
+hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
+  const size_t lds = decompress_lds_bytes(kSvcMaxIn, kSvcMaxOut);
+  hipLaunchKernelGGL(lz4_decode_service_kernel, dim3(1), dim3(64), lds, st, box, idle_ticks, life_ticks);
+  return hipGetLastError();
+}
 
 hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out,

@@ -1,0 +1,103 @@
+"""GPU: the resident decode service of the per-call path (kingdb_amd/csrc/
+service.h): LZ4_decompress_safe_partial (lz4.cc:1050-1053) one block per
+call, served by a wave that stays on the device between calls.
+
+Parity is the batch decoder's (the same decode_block): every return code of
+the reference's malformed-block fixtures at the per-call sizes
+(tests/golden/malformed.npz), and outputs equal to the oracle's, from one
+thread and from 16 threads at once; the wave leaves once idle, and the
+KDB_LZ4_SERVICE=0 build path (one launch per call) gives the same results.
+"""
+import ctypes
+import os
+import random
+import subprocess
+import sys
+import threading
+import time
+
+import pytest
+
+import oracle
+from conftest import ROOT, load_golden, split
+
+pytestmark = pytest.mark.gpu
+
+SMALL = 8192   # the service's class (service.h kSvcMaxOut)
+
+
+def _stats(gpu, dev=0):
+    from kingdb_amd import _lib
+    a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    assert _lib.load().kdb_lz4_service_stats(dev, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
+    return a.value, b.value, c.value
+
+
+def test_service_malformed_codes(gpu):
+    g = load_golden("malformed.npz")
+    blocks = split(g["blk"], g["blk_off"], g["blk_len"])
+    n = 0
+    for i, b in enumerate(blocks):
+        size, tgt = int(g["size"][i]), int(g["target"][i])
+        if size > SMALL or len(b) > SMALL + SMALL // 255 + 24:
+            continue
+        r, out = gpu.decompress_safe_partial(b, tgt, size)
+        assert r == int(g["ret"][i]), (i, r, int(g["ret"][i]))
+        if r > 0 and g["cmp"][i]:
+            o = int(g["out_off"][i])
+            assert out == g["out"][o:o + r].tobytes(), i
+        n += 1
+    launches, served, alive = _stats(gpu)
+    assert n > 1000 and launches >= 1, (n, launches)
+
+
+def test_service_g1_and_random(gpu, orc):
+    rng = random.Random(9)
+    pool = oracle.g1_pool(orc)
+    vals = oracle.g1_values(pool, 100, 300) + oracle.g1_values(pool, 4096, 100) + [b"", b"a" * 13, b"q" * 8192]
+    vals += [bytes(rng.randrange(256) for _ in range(rng.randrange(1, 8192))) for _ in range(20)]
+    t0 = time.perf_counter()
+    for v in vals:
+        b = orc.compress(v)
+        assert gpu.decompress_safe_partial(b, len(v), len(v)) == (len(v), v)
+    dt = (time.perf_counter() - t0) / len(vals) * 1e6
+    print(f"{len(vals)} calls, {dt:.1f} us per call (python included)")
+    time.sleep(0.05)   # idle: the wave has left (KDB_LZ4_SERVICE_IDLE_US, 2 ms)
+    launches, served, alive = _stats(gpu)
+    assert alive == 0 and served >= len(vals), (launches, served, alive)
+
+
+def test_service_many_threads(gpu, orc):
+    pool = oracle.g1_pool(orc)
+    vals = oracle.g1_values(pool, 100, 64) + oracle.g1_values(pool, 4096, 64)
+    blocks = [orc.compress(v) for v in vals]
+    bad = []
+
+    def worker(t):
+        gpu.set_device(0)
+        rng = random.Random(t)
+        for _ in range(300):
+            i = rng.randrange(len(vals))
+            r = gpu.decompress_safe_partial(blocks[i], len(vals[i]), len(vals[i]))
+            if r != (len(vals[i]), vals[i]):
+                bad.append((t, i))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not bad, bad[:5]
+
+
+def test_service_off_is_the_launch_path(gpu, orc):
+    code = ("import sys; sys.path.insert(0, %r); import kingdb_amd as K, oracle, ctypes; "
+            "from kingdb_amd import _lib; K.set_device(0); o = oracle.Oracle(); "
+            "v = oracle.g1_values(oracle.g1_pool(o), 4096, 20); "
+            "assert all(K.decompress_safe_partial(o.compress(x), 4096, 4096) == (4096, x) for x in v); "
+            "a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32(); "
+            "_lib.load().kdb_lz4_service_stats(0, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)); "
+            "assert a.value == 0, a.value; print('ok')") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, KDB_LZ4_SERVICE="0"))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
