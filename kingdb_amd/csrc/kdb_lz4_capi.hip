@@ -31,6 +31,7 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
 hipError_t launch_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed,
                          hipStream_t st);
 hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
+hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
 }  // namespace kdb_lz4
 
 using namespace kdb_lz4;
@@ -139,7 +140,8 @@ inline Meta read_meta(const uint8_t* p) {
   return m;
 }
 
-// ---- the resident decode service (service.h), one per device and process.
+// ---- the resident services (service.h): per device and process, one wave
+// for per-call decodes and one for per-call compressions.
 // KDB_LZ4_SERVICE=0 turns it off (every call launches, as before);
 // KDB_LZ4_SERVICE_IDLE_US (default 2000) is how long the wave waits for the
 // next request before it exits.
@@ -151,8 +153,10 @@ bool service_on() {
   return on;
 }
 
+enum SvcKind { kSvcDecode = 0, kSvcCompress = 1 };
 struct Service {
   std::mutex mu;
+  int kind = kSvcDecode;
   hipStream_t stream = nullptr;
   SvcBox* box = nullptr;     // host view (pinned, coherent, mapped)
   SvcBox* dbox = nullptr;    // its device address
@@ -162,7 +166,9 @@ struct Service {
   int device = 0;
   bool launch() {            // (mu held) a new instance, behind any old one on the stream
     __atomic_store_n(&box->alive, 1u, __ATOMIC_SEQ_CST);
-    if (launch_decode_service(stream, dbox, idle_ticks, life_ticks) != hipSuccess) {
+    const hipError_t e = kind == kSvcDecode ? launch_decode_service(stream, dbox, idle_ticks, life_ticks)
+                                            : launch_compress_service(stream, dbox, idle_ticks, life_ticks);
+    if (e != hipSuccess) {
       __atomic_store_n(&box->alive, 0u, __ATOMIC_SEQ_CST);
       return false;
     }
@@ -195,14 +201,17 @@ void stop_services() {
   }
 }
 
-Service* service_of(int dev) {
+// services()[2 * device + kind]
+Service* service_of(int dev, int kind) {
   std::lock_guard<std::mutex> l(g_svc_mu);
   std::vector<Service*>& v = services();
-  if ((int)v.size() <= dev) v.resize(dev + 1, nullptr);
-  if (v[dev]) return v[dev]->ok ? v[dev] : nullptr;
+  const size_t at = 2u * (size_t)dev + (size_t)kind;
+  if (v.size() <= at) v.resize(at + 1, nullptr);
+  if (v[at]) return v[at]->ok ? v[at] : nullptr;
   Service* s = new Service();
-  v[dev] = s;
+  v[at] = s;
   s->device = dev;
+  s->kind = kind;
   void* h = nullptr;
   int rate_khz = 0;
   if (hipHostMalloc(&h, sizeof(SvcBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
@@ -229,7 +238,7 @@ Service* service_of(int dev) {
 // A calling thread's slot in a device's mailbox, returned when the thread
 // exits; -1 when all 64 are taken (the call launches instead).
 struct SlotLease {
-  std::unordered_map<int, int> slot;   // device -> slot (-1: none)
+  std::unordered_map<int, int> slot;   // 2 * device + kind -> slot (-1: none)
   ~SlotLease() {
     for (auto& kv : slot) {
       Service* s = services().size() > (size_t)kv.first ? services()[kv.first] : nullptr;
@@ -242,7 +251,8 @@ struct SlotLease {
 thread_local SlotLease t_lease;
 int slot_of(Service* s) {
   SlotLease& lease = t_lease;
-  auto it = lease.slot.find(s->device);
+  const int key = 2 * s->device + s->kind;
+  auto it = lease.slot.find(key);
   if (it != lease.slot.end()) return it->second;
   int k = -1;
   {
@@ -252,26 +262,28 @@ int slot_of(Service* s) {
       s->free_slots.pop_back();
     }
   }
-  lease.slot[s->device] = k;
+  lease.slot[key] = k;
   return k;
 }
 
-// One LZ4_decompress_safe_partial through the service; false when it could
-// not be used (no service, no free slot, no answer within a second -- the
-// caller then launches as before).  *ret = the kernel's return word.
-bool service_decode(const char* source, char* dest, uint32_t C, uint32_t O, int target, int* ret) {
+// One call through a service: the slot's arguments (csize = input bytes,
+// osize = output capacity, target) and input; false when it could not be
+// used (no service, no free slot, no answer within a second -- the caller
+// then launches as before).  *ret = the kernel's return word, the output
+// copied to dest when it is > 0.
+bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uint32_t cap, int target, int* ret) {
   if (!service_on()) return false;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
-  Service* s = service_of(dev);
+  Service* s = service_of(dev, kind);
   if (!s) return false;
   const int k = slot_of(s);
   if (k < 0) return false;
   SvcSlot& sl = s->box->slot[k];
-  sl.csize = C;
-  sl.osize = O;
+  sl.csize = in_len;
+  sl.osize = cap;
   sl.target = (uint32_t)target;
-  if (C) memcpy(sl.in, source, C);
+  if (in_len) memcpy(sl.in, source, in_len);
   const uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
   __atomic_store_n(&s->box->req[k], want, __ATOMIC_RELEASE);     // the doorbell, after the arguments
   __atomic_thread_fence(__ATOMIC_SEQ_CST);                        // ... and before alive is read
@@ -286,7 +298,7 @@ bool service_decode(const char* source, char* dest, uint32_t C, uint32_t O, int 
       if (waited > std::chrono::seconds(1)) {
         // no answer (the device busy past a second?): this thread gives the
         // slot up for good (the wave may still write it) and launches
-        t_lease.slot[s->device] = -1;
+        t_lease.slot[2 * s->device + s->kind] = -1;
         return false;
       }
     }
@@ -307,11 +319,14 @@ int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint
   *launches = *served = *alive = 0;
   std::lock_guard<std::mutex> l(g_svc_mu);
   const std::vector<Service*>& v = services();
-  const Service* s = (size_t)device < v.size() ? v[device] : nullptr;
-  if (!s || !s->ok) return KDB_LZ4_OK;
-  *launches = __atomic_load_n(&s->box->launches, __ATOMIC_ACQUIRE);
-  *served = __atomic_load_n(&s->box->served, __ATOMIC_ACQUIRE);
-  *alive = __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE);
+  for (size_t kind = 0; kind < 2; kind++) {
+    const size_t at = 2u * (size_t)device + kind;
+    const Service* s = at < v.size() ? v[at] : nullptr;
+    if (!s || !s->ok) continue;
+    *launches += __atomic_load_n(&s->box->launches, __ATOMIC_ACQUIRE);
+    *served += __atomic_load_n(&s->box->served, __ATOMIC_ACQUIRE);
+    *alive += __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE);
+  }
   return KDB_LZ4_OK;
 }
 
@@ -483,6 +498,11 @@ int kdb_lz4_compress_limitedOutput(const char* source, char* dest, int inputSize
   Meta m{};
   m.len = S;
   m.cap = (uint32_t)maxOutputSize;
+  if (S <= 4096u && cap <= kSvcOutBytes && lane_order_ok() == hipSuccess) {   // the resident compress service
+    int sret = 0;
+    if (service_call(kSvcCompress, source, S, dest, cap, 0, &sret))
+      return sret > 0 && sret != KDB_LZ4_VALUE_UNSUPPORTED ? sret : 0;
+  }
   if (S <= kZeroCopyMax) {                       // zero-copy: [meta][in][out] in mapped host memory
     const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)S + 16);
     if (c.reserve(out_at + align16(cap + 16), 0) != KDB_LZ4_OK) return 0;
@@ -536,7 +556,8 @@ int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compress
   const bool zc = O <= kZeroCopyMax && C <= kZeroCopyMax + kZeroCopyMax / 255u + 24u;
   if (zc && C <= kSvcMaxIn && O <= kSvcMaxOut) {   // the resident decode service (service.h)
     int sret = 0;
-    if (service_decode(source, dest, C, O, targetOutputSize, &sret)) return sret == KDB_LZ4_VALUE_UNSUPPORTED ? -1 : sret;
+    if (service_call(kSvcDecode, source, C, dest, O, targetOutputSize, &sret))
+      return sret == KDB_LZ4_VALUE_UNSUPPORTED ? -1 : sret;
   }
   if (zc) {                                      // zero-copy: [meta][in][out] in mapped host memory
     const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)C + 16);

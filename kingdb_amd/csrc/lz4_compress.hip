@@ -36,6 +36,7 @@
 #include <type_traits>
 
 #include "lz4_device.h"
+#include "service.h"
 
 namespace kdb_lz4 {
 
@@ -837,6 +838,90 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
   values_loop<kFrame, kSmall>(kSmall ? smem_s : smem_d, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                               dst_cap, frame_len, ret, work, batch, nq);
+}
+
+// ---------------------------------------------------------------------------
+// The resident compress service (service.h; lz4_decompress.hip has its decode
+// twin): one wave serving per-call LZ4_compress_limitedOutput requests
+// (lz4.cc:664-682) of values up to kSmallMax bytes from a mailbox in pinned
+// host memory -- the value staged at LDS address 0 next to the Table12 planes,
+// as lz4_compress_kernel<false, true> stages it, the block written straight to
+// the slot in host memory.  Every wave reaches an exit: idle_ticks without a
+// request, life_ticks in all, or the host's stop.
+__device__ __forceinline__ uint32_t csys_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t csys_peek(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, uint64_t idle_ticks,
+                                                                  uint64_t life_ticks) {
+  __shared__ __attribute__((aligned(16))) uint8_t smem_s[kTable12Bytes + kSmallMax];   // the kernel's only LDS
+  const uint32_t lane = lane_id();
+  uint8_t* s_tab = smem_s + kT12Lo;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  for (uint32_t i = lane; i < kTable12Bytes / 16u; i += 64u) reinterpret_cast<uint4*>(s_tab)[i] = z4;
+  __syncthreads();
+  Table12 tab;
+  uint32_t seen = csys_load(&box->done[lane]);
+  const uint64_t t0 = wall_clock64();
+  uint64_t t_last = t0;
+  uint32_t served = 0;
+#pragma unroll 1
+  for (;;) {
+    const uint32_t r = csys_load(&box->req[lane]);
+    uint64_t pend = ballot(r != seen);
+    if (pend == 0) {
+      const uint64_t now = wall_clock64();
+      const bool stop = csys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
+      if (stop || old || now - t_last > idle_ticks) {
+        if (lane == 0) __hip_atomic_store(&box->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        const uint32_t r2 = csys_load(&box->req[lane]);
+        if (stop || old || ballot(r2 != seen) == 0) break;
+        if (lane == 0) __hip_atomic_store(&box->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(4);
+      continue;
+    }
+#pragma unroll 1
+    while (pend) {
+      const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1u;
+      const uint32_t want = readlane(r, sidx);
+      SvcSlot* sl = &box->slot[sidx];
+      const uint32_t S = uni(csys_peek(&sl->csize)), cap = uni(csys_peek(&sl->osize));
+      int rc = (int)kUnsupported;
+      if (S <= kSmallMax && cap <= kSvcOutBytes) {
+        stage_aligned(sl->in, S, smem_s);              // the value at LDS [0, S)
+        __syncthreads();
+        const uint32_t bound = compress_bound(S);
+        LdsSrc ls{smem_s};
+        rc = cap < bound ? compress_block<false, true>(ls, S, tab, sl->out, (int)cap, (int)cap)
+                         : compress_block<false, false>(ls, S, tab, sl->out, (int)bound, (int)cap);
+#pragma unroll
+        for (uint32_t k = 0; k < kTable12Bytes / 1024u; ++k) reinterpret_cast<uint4*>(s_tab)[lane + 64u * k] = z4;
+        __syncthreads();
+      }
+      if (lane == 0) {
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(&sl->ret), (uint32_t)rc, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&box->done[sidx], want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (lane == sidx) seen = want;
+      served++;
+    }
+    t_last = wall_clock64();
+  }
+  if (lane == 0)
+    __hip_atomic_store(&box->served, csys_peek(&box->served) + served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
+  hipLaunchKernelGGL(lz4_compress_service_kernel, dim3(1), dim3(64), 0, st, box, idle_ticks, life_ticks);
+  return hipGetLastError();
 }
 
 // LDS bytes a launch needs for values up to max_len bytes.

@@ -1,12 +1,14 @@
-"""GPU: the resident decode service of the per-call path (kingdb_amd/csrc/
-service.h): LZ4_decompress_safe_partial (lz4.cc:1050-1053) one block per
-call, served by a wave that stays on the device between calls.
+"""GPU: the resident services of the per-call path (kingdb_amd/csrc/
+service.h): LZ4_decompress_safe_partial (lz4.cc:1050-1053) and
+LZ4_compress_limitedOutput (lz4.cc:664-682) one value per call, served by
+waves that stay on the device between calls.
 
-Parity is the batch decoder's (the same decode_block): every return code of
-the reference's malformed-block fixtures at the per-call sizes
-(tests/golden/malformed.npz), and outputs equal to the oracle's, from one
-thread and from 16 threads at once; the wave leaves once idle, and the
-KDB_LZ4_SERVICE=0 build path (one launch per call) gives the same results.
+Parity is the batch kernels' (the same decode_block / compress_block): every
+return code of the reference's malformed-block fixtures at the per-call sizes
+(tests/golden/malformed.npz), the reference's limited-output return codes and
+blocks (limited_output.npz), outputs equal to the oracle's, from one thread
+and from 16 threads at once; the waves leave once idle, and with
+KDB_LZ4_SERVICE=0 (one launch per call) the results are the same.
 """
 import ctypes
 import os
@@ -67,6 +69,28 @@ def test_service_g1_and_random(gpu, orc):
     assert alive == 0 and served >= len(vals), (launches, served, alive)
 
 
+def test_service_compress_limited_output(gpu, orc):
+    """The reference's limitedOutput return codes and blocks (values <= 4 KiB
+    go to the compress service), and the G1 values at the bound."""
+    g = load_golden("limited_output.npz")
+    inputs = split(g["inp"], g["inp_off"], g["inp_len"])
+    n = 0
+    for i, x in enumerate(inputs):
+        cap = int(g["cap"][i])
+        r, b = gpu.compress_limited_output(x, cap)
+        assert r == int(g["ret"][i]), (i, r, int(g["ret"][i]))
+        if r:
+            o = int(g["blk_off"][i])
+            assert b == g["blk"][o:o + r].tobytes(), i
+        n += len(x) <= 4096
+    pool = oracle.g1_pool(orc)
+    for x in oracle.g1_values(pool, 100, 200) + oracle.g1_values(pool, 4096, 50) + [b"", b"a", b"a" * 13]:
+        r, b = gpu.compress_limited_output(x, orc.compress_bound(len(x)))
+        assert b == orc.compress(x), len(x)
+    launches, served, alive = _stats(gpu)
+    assert n > 100 and launches >= 1, (n, launches)
+
+
 def test_service_many_threads(gpu, orc):
     pool = oracle.g1_pool(orc)
     vals = oracle.g1_values(pool, 100, 64) + oracle.g1_values(pool, 4096, 64)
@@ -81,6 +105,9 @@ def test_service_many_threads(gpu, orc):
             r = gpu.decompress_safe_partial(blocks[i], len(vals[i]), len(vals[i]))
             if r != (len(vals[i]), vals[i]):
                 bad.append((t, i))
+            c = gpu.compress_limited_output(vals[i], len(vals[i]) + len(vals[i]) // 255 + 16)
+            if c[1] != blocks[i]:
+                bad.append((t, i, "compress"))
 
     th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
     for t in th:
