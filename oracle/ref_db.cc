@@ -32,6 +32,8 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <random>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -137,8 +139,61 @@ static int verify(int argc, char** argv) {
   return bad || it_bad || mp_bad ? 1 : 0;
 }
 
+// ref_db --readrandom <dbdir> <keys> <reads> <threads> [maximum_part_size [hstable_size [hash]]]:
+// db_bench's ReadRandom (/root/reference/doc/bench/db_bench_kingdb.cc:505-518)
+// on a database already written (keys "%016d" of 0 .. keys-1): <threads>
+// client threads share <reads> Database::Get calls of uniformly random keys
+// (std::mt19937 per thread: the reference's leveldb Random is not vendored),
+// ReadOptions defaults.  Prints reads/s, the values found and their bytes.
+static int readrandom(int argc, char** argv) {
+  const char* dir = argv[2];
+  const long keys = atol(argv[3]), reads = atol(argv[4]);
+  const int threads = atoi(argv[5]);
+  kdb::Logger::set_current_level("emerg");
+  kdb::DatabaseOptions options;
+  if (argc > 6) options.storage__maximum_part_size = strtoull(argv[6], nullptr, 0);
+  if (argc > 7) options.storage__hstable_size = strtoull(argv[7], nullptr, 0);
+  if (argc > 8) options.hash = strtoul(argv[8], nullptr, 0) ? kdb::kxxHash_64 : kdb::kMurmurHash3_64;
+  kdb::Database db(options, dir);
+  kdb::Status s = db.Open();
+  if (!s.IsOK()) {
+    fprintf(stderr, "open: %s\n", s.ToString().c_str());
+    return 1;
+  }
+  std::vector<uint64_t> found(threads, 0), bytes(threads, 0);
+  std::vector<std::thread> th;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t] {
+      std::mt19937_64 rng(301 + t);
+      kdb::ReadOptions ro;
+      const long n = reads / threads + (t < reads % threads ? 1 : 0);
+      for (long i = 0; i < n; i++) {
+        char key[100];
+        snprintf(key, sizeof(key), "%016d", (int)(rng() % (uint64_t)keys));
+        std::string value;
+        if (db.Get(ro, key, &value).IsOK()) {
+          found[t]++;
+          bytes[t] += value.size();
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  uint64_t f = 0, b = 0;
+  for (int t = 0; t < threads; t++) {
+    f += found[t];
+    b += bytes[t];
+  }
+  db.Close();
+  printf("readrandom %ld reads %d threads %.6f s %.1f reads_per_s found %llu bytes %llu\n", reads, threads, sec,
+         reads / sec, (unsigned long long)f, (unsigned long long)b);
+  return f == (uint64_t)reads ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 4 && !strcmp(argv[1], "--verify")) return verify(argc, argv);
+  if (argc >= 6 && !strcmp(argv[1], "--readrandom")) return readrandom(argc, argv);
   if (argc < 3) {
     fprintf(stderr, "usage: ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash [none]]]]\n");
     return 2;
