@@ -381,6 +381,12 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     const int key_match = lane <= 1u ? INT32_MAX : lane == 2u ? INT32_MIN : (int)lane;
     // The rest of a sequence once its search found a match (mm: the matching
     // lanes, pk/refk/slot: the chunk's positions, entries and table slots).
+#if KDB_C_HOIST_K
+    // (A/B variant) the count's out-of-range markers made opaque once, kept in
+    // two VGPRs across the sequence loop instead of rebuilt per sequence
+    uint32_t k256h = 256u, k257h = 257u;
+    asm volatile("" : "+v"(k256h), "+v"(k257h));
+#endif
     auto finish = [&](uint64_t mm, uint32_t pk, uint32_t refk, const typename Tab::Slot& slot) {
       const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
       uint32_t ip = readlane(pk, ks);
@@ -401,6 +407,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml, ip_end;
+#if KDB_C_EARLY_LIT
+      uint32_t lb_early = 0;
+#endif
       {
         // catch-up bound (lz4.cc:531: ip > anchor, ref > base): 0 for a
         // lane-2 match of a lead chunk (ip == anchor), the _next_match path
@@ -413,6 +422,15 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         const uint32_t a0 = src.u8(clamp1(ia)), b0 = src.u8(clamp1(ra));
         const uint32_t a1 = src.u8(clamp1(ib));
         const uint32_t b1 = src.u8(clamp1(ref + kMinMatch + lane));
+#if KDB_C_EARLY_LIT
+        // (A/B variant) the literal byte of this lane's place in the encoding,
+        // read now, with the count's bytes, for the case without catch-up (c
+        // == 0: lit = ip - anchor); the emission re-reads it otherwise
+        if constexpr (kFree) {
+          const uint32_t lit0 = ip - anchor;
+          lb_early = src.u8((lane - 1u) - ((lit0 + 241u) >> 8) + anchor);
+        }
+#endif
         // in-place values: the restore (table writes) goes out behind the
         // count's reads (value bytes in HBM, no overlap), so their issue does
         // not wait behind it; it lands before the next sequence's exchange
@@ -433,8 +451,12 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // the read addresses on the vector unit, selects rather than an AND of
         // masks on the CU's one scalar unit (the 256 is opaque so the compiler
         // does not fold the selects back into one)
+#if KDB_C_HOIST_K
+        const uint32_t k256 = k256h, k257 = k257h;
+#else
         uint32_t k256 = 256u, k257 = 257u;           // two, so the nested selects stay two
         asm volatile("" : "+v"(k256), "+v"(k257));
+#endif
         // (in-place values, whose reads are clamped, compare the lane with
         // lim and rem: measured a little faster there)
         const uint32_t x0 = kFree ? ((int)ra >= 0 ? ((int)ia >= (int)anchor ? a0 : k256) : k257)
@@ -542,7 +564,16 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         uint32_t lb;
         if constexpr (!kWin) {
           seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+#if KDB_C_EARLY_LIT
+          if constexpr (kFree) {
+            lb = lb_early;
+            if (__builtin_expect(c != 0u, 0)) lb = src.u8(clamp1(seq_anchor + da));
+          } else {
+            lb = src.u8(clamp1(seq_anchor + da));
+          }
+#else
           lb = src.u8(clamp1(seq_anchor + da));
+#endif
         } else {
           // next input words: bytes ip_end - 2 + lane .. +3, at window offset
           // ml + 2 + lane (ml before the catch-up); covered while ml <= 187
