@@ -224,7 +224,8 @@ Service* service_of(int dev, int kind) {
   const char* e = getenv("KDB_LZ4_SERVICE_IDLE_US");
   const uint64_t idle_us = e && *e ? strtoull(e, nullptr, 10) : 2000u;
   s->idle_ticks = idle_us * (uint64_t)rate_khz / 1000u;
-  s->life_ticks = 500ull * (uint64_t)rate_khz;   // 500 ms, then a fresh instance
+  s->life_ticks = 20ull * (uint64_t)rate_khz;    // 20 ms, then a fresh instance (bounds how long a
+                                                  // batch launch can wait behind the wave for a slot)
   for (int i = (int)kSvcSlots - 1; i >= 0; i--) s->free_slots.push_back(i);
   static bool registered = false;
   if (!registered) {
@@ -234,6 +235,25 @@ Service* service_of(int dev, int kind) {
   s->ok = true;
   return s;
 }
+
+}  // namespace
+
+namespace kdb_lz4 {
+uint32_t services_resident(int dev) {
+  if (!service_on()) return 0;
+  std::lock_guard<std::mutex> l(g_svc_mu);
+  const std::vector<Service*>& v = services();
+  uint32_t n = 0;
+  for (size_t kind = 0; kind < 2; kind++) {
+    const size_t at = 2u * (size_t)dev + kind;
+    const Service* s = at < v.size() ? v[at] : nullptr;
+    if (s && s->ok && __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE)) n++;
+  }
+  return n;
+}
+}  // namespace kdb_lz4
+
+namespace {
 
 // A calling thread's slot in a device's mailbox, returned when the thread
 // exits; -1 when all 64 are taken (the call launches instead).

@@ -124,6 +124,12 @@ uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
   static const bool dbg = kdb_tune("KDB_LZ4_DEBUG", 0) != 0;
   if (dbg) fprintf(stderr, "persistent_grid: lds=%zu per_cu=%d cus=%d\n", lds, per_cu, cus);
   uint64_t slots = (uint64_t)per_cu * (uint64_t)cus;
+  // a resident service wave (service.h) holds a wave slot and LDS on some CU
+  // for as long as calls keep coming: a grid that counted on that CU's full
+  // capacity would leave a workgroup waiting behind it, and the launch's tail
+  // with it, so each one resident on this device takes a margin off the grid
+  const uint32_t svc = services_resident(dev);
+  if (svc) slots = slots > 8u * svc + 1u ? slots - 8u * svc : 1u;
   return (uint32_t)(n < slots ? n : slots);
 }
 

@@ -200,6 +200,8 @@ hipError_t work_counter(hipStream_t st, uint32_t** ctr);
 // against reuse (launch_util.hip)
 hipError_t work_counter_release(hipStream_t st, uint32_t* ctr);
 uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
+// service waves (service.h) resident on `dev` right now (kdb_lz4_capi.hip)
+uint32_t services_resident(int dev);
 // The launch's work counter: a direct launch (n no larger than the resident
 // grid, so one value per workgroup) needs none (*ctr = nullptr, no memset:
 // the scalar entry points' latency); otherwise a zeroed counter slot.
