@@ -109,6 +109,8 @@ hipError_t launch_counter(hipStream_t st, uint32_t n, uint32_t grid, uint32_t** 
   return work_counter(st, ctr);
 }
 
+uint32_t services_resident(int dev);   // kdb_lz4_capi.hip (service.h)
+
 // Workgroups of 64 threads resident at once for `kern` with `lds` bytes of
 // dynamic LDS, capped at n (the kernels dequeue values dynamically, so a
 // workgroup that is admitted late simply takes fewer values).
