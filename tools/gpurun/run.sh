@@ -21,6 +21,7 @@
 #   hook       the flush-hook build's tests only (test_kingdb_dropin.py -k hook)
 #   wpath      KingDB's write path (kdb_db) with the reference codec, the drop-in and
 #              the flush hook, 1 M x 100 B + 128 Ki x 4 KiB, on /tmp and on /dev/shm
+#   readrandom db_bench readrandom through KingDB (reference codec, drop-in, hook; 1 and 16 threads)
 #   rehearse2  the four bench workloads under torch.distributed.run with 2 ranks on this
 #              1-GPU box (ranks share the device): the N > 1 path end to end, not scaling
 #   scalar     per-call latency of CompressorLZ4::Compress/Uncompress, drop-in vs reference
@@ -100,6 +101,9 @@ for s in "$@"; do
         timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port $port bench.py --gpus 2 --workload $w --no-cpu-baseline > "${O}_rehearse2_$w.json" 2> "${O}_rehearse2_$w.err" || fail "rehearse2 $w" $? "${O}_rehearse2_$w.err"
         line "${O}_rehearse2_$w.json"
       done ;;
+    readrandom)   # db_bench readrandom through KingDB: reference codec, drop-in, hook; 1 and 16 threads
+      timeout -k 10 900 python -u tools/readrandom_cmp.py --out "${O}_readrandom.json" > "${O}_readrandom.log" 2>&1 || fail readrandom $? "${O}_readrandom.log"
+      cat "${O}_readrandom.log" ;;
     scalar)   # per-call latency of CompressorLZ4, drop-in (GPU) vs reference codec (CPU)
       for sz in 100 4096 65536; do
         for v in kingdb_ref kingdb_dropin; do
