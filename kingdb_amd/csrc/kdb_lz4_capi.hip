@@ -300,17 +300,20 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   const int k = slot_of(s);
   if (k < 0) return false;
   SvcSlot& sl = s->box->slot[k];
-  sl.csize = in_len;
-  sl.osize = cap;
-  sl.target = (uint32_t)target;
+  SvcArgs& a = s->box->args[k];
+  a.csize = in_len;
+  a.osize = cap;
+  a.target = (uint32_t)target;
   if (in_len) memcpy(sl.in, source, in_len);
   const uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
   __atomic_store_n(&s->box->req[k], want, __ATOMIC_RELEASE);     // the doorbell, after the arguments
   __atomic_thread_fence(__ATOMIC_SEQ_CST);                        // ... and before alive is read
   s->ensure_running();
   const auto t0 = std::chrono::steady_clock::now();
+  uint64_t done = 0;
   for (uint32_t spins = 1;; spins++) {
-    if (__atomic_load_n(&s->box->done[k], __ATOMIC_ACQUIRE) == want) break;
+    done = __atomic_load_n(&s->box->done[k], __ATOMIC_ACQUIRE);
+    if ((uint32_t)(done >> 32) == want) break;
     __builtin_ia32_pause();
     if ((spins & 1023u) == 0) {
       const auto waited = std::chrono::steady_clock::now() - t0;
@@ -323,7 +326,7 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
       }
     }
   }
-  *ret = __atomic_load_n(&sl.ret, __ATOMIC_ACQUIRE);
+  *ret = (int32_t)(uint32_t)done;
   if (*ret > 0) memcpy(dest, sl.out, (size_t)*ret);
   return true;
 }

@@ -381,12 +381,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     const int key_match = lane <= 1u ? INT32_MAX : lane == 2u ? INT32_MIN : (int)lane;
     // The rest of a sequence once its search found a match (mm: the matching
     // lanes, pk/refk/slot: the chunk's positions, entries and table slots).
-#if KDB_C_HOIST_K
-    // (A/B variant) the count's out-of-range markers made opaque once, kept in
-    // two VGPRs across the sequence loop instead of rebuilt per sequence
-    uint32_t k256h = 256u, k257h = 257u;
-    asm volatile("" : "+v"(k256h), "+v"(k257h));
-#endif
     auto finish = [&](uint64_t mm, uint32_t pk, uint32_t refk, const typename Tab::Slot& slot) {
       const uint32_t ks = (uint32_t)__builtin_ctzll(mm);
       uint32_t ip = readlane(pk, ks);
@@ -407,9 +401,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
 
       // ======== catch up (lz4.cc:531) and LZ4_count (lz4.cc:562-578), issued together
       uint32_t c, ml, ip_end;
-#if KDB_C_EARLY_LIT
-      uint32_t lb_early = 0;
-#endif
       {
         // catch-up bound (lz4.cc:531: ip > anchor, ref > base): 0 for a
         // lane-2 match of a lead chunk (ip == anchor), the _next_match path
@@ -422,15 +413,6 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         const uint32_t a0 = src.u8(clamp1(ia)), b0 = src.u8(clamp1(ra));
         const uint32_t a1 = src.u8(clamp1(ib));
         const uint32_t b1 = src.u8(clamp1(ref + kMinMatch + lane));
-#if KDB_C_EARLY_LIT
-        // (A/B variant) the literal byte of this lane's place in the encoding,
-        // read now, with the count's bytes, for the case without catch-up (c
-        // == 0: lit = ip - anchor); the emission re-reads it otherwise
-        if constexpr (kFree) {
-          const uint32_t lit0 = ip - anchor;
-          lb_early = src.u8((lane - 1u) - ((lit0 + 241u) >> 8) + anchor);
-        }
-#endif
         // in-place values: the restore (table writes) goes out behind the
         // count's reads (value bytes in HBM, no overlap), so their issue does
         // not wait behind it; it lands before the next sequence's exchange
@@ -451,12 +433,8 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // the read addresses on the vector unit, selects rather than an AND of
         // masks on the CU's one scalar unit (the 256 is opaque so the compiler
         // does not fold the selects back into one)
-#if KDB_C_HOIST_K
-        const uint32_t k256 = k256h, k257 = k257h;
-#else
         uint32_t k256 = 256u, k257 = 257u;           // two, so the nested selects stay two
         asm volatile("" : "+v"(k256), "+v"(k257));
-#endif
         // (in-place values, whose reads are clamped, compare the lane with
         // lim and rem: measured a little faster there)
         const uint32_t x0 = kFree ? ((int)ra >= 0 ? ((int)ia >= (int)anchor ? a0 : k256) : k257)
@@ -564,16 +542,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         uint32_t lb;
         if constexpr (!kWin) {
           seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
-#if KDB_C_EARLY_LIT
-          if constexpr (kFree) {
-            lb = lb_early;
-            if (__builtin_expect(c != 0u, 0)) lb = src.u8(clamp1(seq_anchor + da));
-          } else {
-            lb = src.u8(clamp1(seq_anchor + da));
-          }
-#else
           lb = src.u8(clamp1(seq_anchor + da));
-#endif
         } else {
           // next input words: bytes ip_end - 2 + lane .. +3, at window offset
           // ml + 2 + lane (ml before the catch-up); covered while ml <= 187
@@ -895,38 +864,22 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
   for (uint32_t i = lane; i < kTable12Bytes / 16u; i += 64u) reinterpret_cast<uint4*>(s_tab)[i] = z4;
   __syncthreads();
   Table12 tab;
-  uint32_t seen = csys_load(&box->done[lane]);
+  uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
   uint32_t served = 0;
-#pragma unroll 1
-  for (;;) {
-    const uint32_t r = csys_load(&box->req[lane]);
-    uint64_t pend = ballot(r != seen);
-    if (pend == 0) {
-      const uint64_t now = wall_clock64();
-      const bool stop = csys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
-      if (stop || old || now - t_last > idle_ticks) {
-        if (lane == 0) __hip_atomic_store(&box->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-        __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        const uint32_t r2 = csys_load(&box->req[lane]);
-        if (stop || old || ballot(r2 != seen) == 0) break;
-        if (lane == 0) __hip_atomic_store(&box->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-        continue;
-      }
-      __builtin_amdgcn_s_sleep(4);
-      continue;
-    }
+  // serves every slot of `pend` (their doorbells read as r)
+  auto serve = [&](uint64_t pend, uint32_t r) {
 #pragma unroll 1
     while (pend) {
       const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1u;
       const uint32_t want = readlane(r, sidx);
       SvcSlot* sl = &box->slot[sidx];
-      const uint32_t S = uni(csys_peek(&sl->csize)), cap = uni(csys_peek(&sl->osize));
+      const SvcArgs a = svc_fetch(box, sidx, smem_s, kSmallMax);   // the value at LDS [0, S)
+      const uint32_t S = a.csize, cap = a.osize;
       int rc = (int)kUnsupported;
       if (S <= kSmallMax && cap <= kSvcOutBytes) {
-        stage_aligned(sl->in, S, smem_s);              // the value at LDS [0, S)
         __syncthreads();
         const uint32_t bound = compress_bound(S);
         LdsSrc ls{smem_s};
@@ -936,14 +889,41 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
         for (uint32_t k = 0; k < kTable12Bytes / 1024u; ++k) reinterpret_cast<uint4*>(s_tab)[lane + 64u * k] = z4;
         __syncthreads();
       }
-      if (lane == 0) {
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(&sl->ret), (uint32_t)rc, __ATOMIC_RELEASE,
+      if (lane == 0)   // after the block: the request and its return value, one store
+        __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&box->done[sidx], want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
       if (lane == sidx) seen = want;
       served++;
     }
+  };
+#pragma unroll 1
+  for (;;) {
+    const uint32_t r = csys_load(&box->req[lane]);   // the 64 doorbells: one 256-byte read
+    const uint64_t pend = ballot(r != seen);
+    if (pend == 0) {
+      const uint64_t now = wall_clock64();
+      const bool stop = csys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
+      if (stop || old || now - t_last > idle_ticks) {
+        // leave: clear alive, then look at the doorbells once more.  A caller
+        // that rang before it read alive sees alive set, so it is served here
+        // (idle: and the wave goes on; at its end of life or at stop: these
+        // last ones, then it leaves); one that rang later sees it clear and
+        // launches the next instance, which queues behind this one.
+        if (lane == 0) __hip_atomic_store(&box->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        const uint32_t r2 = csys_load(&box->req[lane]);
+        const uint64_t pend2 = ballot(r2 != seen);
+        if (pend2 == 0) break;
+        serve(pend2, r2);
+        if (stop || old) break;
+        if (lane == 0) __hip_atomic_store(&box->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+        t_last = wall_clock64();
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    serve(pend, r);
     t_last = wall_clock64();
   }
   if (lane == 0)

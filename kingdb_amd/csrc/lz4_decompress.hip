@@ -955,54 +955,64 @@ __global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uin
   constexpr uint32_t s_in_cap = (kSvcMaxIn + 32u + 15u) & ~15u;   // small_decode_loop's layout
   uint8_t* s_in = smem;
   uint8_t* s_out = smem + s_in_cap;
-  uint32_t seen = sys_load(&box->done[lane]);   // lane i: the last request of slot i served
+  // lane i: the last request of slot i served
+  uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
   uint32_t served = 0;
-#pragma unroll 1
-  for (;;) {
-    const uint32_t r = sys_load(&box->req[lane]);   // the 64 doorbells: one 256-byte read
-    uint64_t pend = ballot(r != seen);
-    if (pend == 0) {
-      const uint64_t now = wall_clock64();
-      const bool stop = sys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
-      if (stop || old || now - t_last > idle_ticks) {
-        // leave: clear alive, then look at the doorbells once more (a caller
-        // that rang before it read alive is served here)
-        if (lane == 0) sys_store(&box->alive, 0u, __ATOMIC_SEQ_CST);
-        __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        const uint32_t r2 = sys_load(&box->req[lane]);
-        if (stop || old || ballot(r2 != seen) == 0) break;
-        if (lane == 0) sys_store(&box->alive, 1u, __ATOMIC_SEQ_CST);
-        continue;
-      }
-      __builtin_amdgcn_s_sleep(4);
-      continue;
-    }
+  // serves every slot of `pend` (their doorbells read as r)
+  auto serve = [&](uint64_t pend, uint32_t r) {
 #pragma unroll 1
     while (pend) {
       const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1u;
       const uint32_t want = readlane(r, sidx);
-      SvcSlot* sl = &box->slot[sidx];
-      const int csize = (int)uni(sys_peek(&sl->csize)), osize = (int)uni(sys_peek(&sl->osize));
-      const int tgt = (int)uni(sys_peek(&sl->target));
+      // the arguments and the block, staged at s_in (head 0)
+      const SvcArgs a = svc_fetch(box, sidx, s_in, kSvcMaxIn);
+      const int csize = (int)a.csize, osize = (int)a.osize, tgt = (int)a.target;
       int rc = (int)kUnsupported;
       if (csize >= 0 && osize >= 0 && (uint32_t)csize <= kSvcMaxIn && (uint32_t)osize <= kSvcMaxOut) {
-        const uint32_t head = stage_to_lds(sl->in, (uint32_t)csize, s_in);
-        if (lane < 16u) s_in[head + (uint32_t)csize + lane] = 0;   // OOB bytes read as 0
+        if (lane < 16u) s_in[(uint32_t)csize + lane] = 0;   // OOB bytes read as 0
         __syncthreads();
-        rc = decode_block(s_in, head, csize, s_out, osize, tgt);
-        if (rc > 0) flush_lds_to_global(sl->out, s_out, 0, (uint32_t)rc);
+        rc = decode_block(s_in, 0u, csize, s_out, osize, tgt);
+        if (rc > 0) flush_lds_to_global(box->slot[sidx].out, s_out, 0, (uint32_t)rc);
         __syncthreads();
       }
-      if (lane == 0) {
-        sys_store(reinterpret_cast<uint32_t*>(&sl->ret), (uint32_t)rc, __ATOMIC_RELEASE);
-        sys_store(&box->done[sidx], want, __ATOMIC_RELEASE);   // after the bytes and ret
-      }
+      if (lane == 0)   // after the bytes: the request and its return value, one store
+        __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       if (lane == sidx) seen = want;
       served++;
     }
+  };
+#pragma unroll 1
+  for (;;) {
+    const uint32_t r = sys_load(&box->req[lane]);   // the 64 doorbells: one 256-byte read
+    const uint64_t pend = ballot(r != seen);
+    if (pend == 0) {
+      const uint64_t now = wall_clock64();
+      const bool stop = sys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
+      if (stop || old || now - t_last > idle_ticks) {
+        // leave: clear alive, then look at the doorbells once more.  A caller
+        // that rang before it read alive sees alive set, so it is served here
+        // (idle: and the wave goes on; at its end of life or at stop: these
+        // last ones, then it leaves); one that rang later sees it clear and
+        // launches the next instance, which queues behind this one.
+        if (lane == 0) sys_store(&box->alive, 0u, __ATOMIC_SEQ_CST);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+        const uint32_t r2 = sys_load(&box->req[lane]);
+        const uint64_t pend2 = ballot(r2 != seen);
+        if (pend2 == 0) break;
+        serve(pend2, r2);
+        if (stop || old) break;
+        if (lane == 0) sys_store(&box->alive, 1u, __ATOMIC_SEQ_CST);
+        t_last = wall_clock64();
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    serve(pend, r);
     t_last = wall_clock64();
   }
   if (lane == 0) sys_store(&box->served, sys_peek(&box->served) + served, __ATOMIC_RELEASE);
