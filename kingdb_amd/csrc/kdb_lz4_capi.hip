@@ -140,11 +140,13 @@ inline Meta read_meta(const uint8_t* p) {
   return m;
 }
 
-// ---- the resident services (service.h): per device and process, one wave
-// for per-call decodes and one for per-call compressions.
-// KDB_LZ4_SERVICE=0 turns it off (every call launches, as before);
-// KDB_LZ4_SERVICE_IDLE_US (default 2000) is how long the wave waits for the
-// next request before it exits.
+// ---- the resident services (service.h): per device and process, up to
+// KDB_LZ4_SERVICE_WAVES (default 4) waves for per-call decodes and as many for
+// per-call compressions, each with a mailbox and a stream of its own; a
+// calling thread is assigned one of them (round robin) with its slot, so
+// concurrent callers are served side by side.  KDB_LZ4_SERVICE=0 turns it
+// off (every call launches, as before); KDB_LZ4_SERVICE_IDLE_US (default
+// 2000) is how long a wave waits for the next request before it exits.
 bool service_on() {
   static const bool on = [] {
     const char* e = getenv("KDB_LZ4_SERVICE");
@@ -154,9 +156,23 @@ bool service_on() {
 }
 
 enum SvcKind { kSvcDecode = 0, kSvcCompress = 1 };
+constexpr int kSvcWavesMax = 8;
+int svc_waves() {
+  static const int n = [] {
+    const char* e = getenv("KDB_LZ4_SERVICE_WAVES");
+    const int v = e && *e ? atoi(e) : 4;
+    return v < 1 ? 1 : (v > kSvcWavesMax ? kSvcWavesMax : v);
+  }();
+  return n;
+}
+// services()[svc_index(device, kind, wave)]
+inline size_t svc_index(int dev, int kind, int wave) {
+  return ((size_t)dev * 2u + (size_t)kind) * (size_t)kSvcWavesMax + (size_t)wave;
+}
 struct Service {
   std::mutex mu;
   int kind = kSvcDecode;
+  int wave = 0;
   hipStream_t stream = nullptr;
   SvcBox* box = nullptr;     // host view (pinned, coherent, mapped)
   SvcBox* dbox = nullptr;    // its device address
@@ -201,17 +217,17 @@ void stop_services() {
   }
 }
 
-// services()[2 * device + kind]
-Service* service_of(int dev, int kind) {
+Service* service_of(int dev, int kind, int wave) {
   std::lock_guard<std::mutex> l(g_svc_mu);
   std::vector<Service*>& v = services();
-  const size_t at = 2u * (size_t)dev + (size_t)kind;
+  const size_t at = svc_index(dev, kind, wave);
   if (v.size() <= at) v.resize(at + 1, nullptr);
   if (v[at]) return v[at]->ok ? v[at] : nullptr;
   Service* s = new Service();
   v[at] = s;
   s->device = dev;
   s->kind = kind;
+  s->wave = wave;
   void* h = nullptr;
   int rate_khz = 0;
   if (hipHostMalloc(&h, sizeof(SvcBox), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
@@ -244,46 +260,57 @@ uint32_t services_resident(int dev) {
   std::lock_guard<std::mutex> l(g_svc_mu);
   const std::vector<Service*>& v = services();
   uint32_t n = 0;
-  for (size_t kind = 0; kind < 2; kind++) {
-    const size_t at = 2u * (size_t)dev + kind;
-    const Service* s = at < v.size() ? v[at] : nullptr;
-    if (s && s->ok && __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE)) n++;
-  }
+  for (int kind = 0; kind < 2; kind++)
+    for (int w = 0; w < kSvcWavesMax; w++) {
+      const size_t at = svc_index(dev, kind, w);
+      const Service* s = at < v.size() ? v[at] : nullptr;
+      if (s && s->ok && __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE)) n++;
+    }
   return n;
 }
 }  // namespace kdb_lz4
 
 namespace {
 
-// A calling thread's slot in a device's mailbox, returned when the thread
-// exits; -1 when all 64 are taken (the call launches instead).
+// A calling thread's wave and slot for a device and kind, the slot returned
+// when the thread exits; slot -1 when every wave's 64 are taken (the call
+// launches instead).
+struct Lease {
+  Service* s;
+  int slot;
+};
 struct SlotLease {
-  std::unordered_map<int, int> slot;   // 2 * device + kind -> slot (-1: none)
+  std::unordered_map<int, Lease> slot;   // 2 * device + kind -> lease
   ~SlotLease() {
     for (auto& kv : slot) {
-      Service* s = services().size() > (size_t)kv.first ? services()[kv.first] : nullptr;
-      if (!s || kv.second < 0) continue;
+      Service* s = kv.second.s;
+      if (!s || kv.second.slot < 0) continue;
       std::lock_guard<std::mutex> l(s->mu);
-      s->free_slots.push_back(kv.second);
+      s->free_slots.push_back(kv.second.slot);
     }
   }
 };
 thread_local SlotLease t_lease;
-int slot_of(Service* s) {
+std::atomic<unsigned> g_next_wave{0};
+Lease lease_of(int dev, int kind) {
   SlotLease& lease = t_lease;
-  const int key = 2 * s->device + s->kind;
+  const int key = 2 * dev + kind;
   auto it = lease.slot.find(key);
   if (it != lease.slot.end()) return it->second;
-  int k = -1;
-  {
+  const int waves = svc_waves();
+  const int first = (int)(g_next_wave.fetch_add(1, std::memory_order_relaxed) % (unsigned)waves);
+  Lease got{nullptr, -1};
+  for (int i = 0; i < waves && got.slot < 0; i++) {
+    Service* s = service_of(dev, kind, (first + i) % waves);
+    if (!s) continue;
     std::lock_guard<std::mutex> l(s->mu);
     if (!s->free_slots.empty()) {
-      k = s->free_slots.back();
+      got = Lease{s, s->free_slots.back()};
       s->free_slots.pop_back();
     }
   }
-  lease.slot[key] = k;
-  return k;
+  lease.slot[key] = got;
+  return got;
 }
 
 // One call through a service: the slot's arguments (csize = input bytes,
@@ -295,10 +322,10 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   if (!service_on()) return false;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
-  Service* s = service_of(dev, kind);
-  if (!s) return false;
-  const int k = slot_of(s);
-  if (k < 0) return false;
+  const Lease ls = lease_of(dev, kind);
+  if (ls.slot < 0) return false;
+  Service* s = ls.s;
+  const int k = ls.slot;
   SvcSlot& sl = s->box->slot[k];
   SvcArgs& a = s->box->args[k];
   a.csize = in_len;
@@ -321,7 +348,7 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
       if (waited > std::chrono::seconds(1)) {
         // no answer (the device busy past a second?): this thread gives the
         // slot up for good (the wave may still write it) and launches
-        t_lease.slot[2 * s->device + s->kind] = -1;
+        t_lease.slot[2 * s->device + s->kind] = Lease{nullptr, -1};
         return false;
       }
     }
@@ -342,14 +369,15 @@ int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint
   *launches = *served = *alive = 0;
   std::lock_guard<std::mutex> l(g_svc_mu);
   const std::vector<Service*>& v = services();
-  for (size_t kind = 0; kind < 2; kind++) {
-    const size_t at = 2u * (size_t)device + kind;
-    const Service* s = at < v.size() ? v[at] : nullptr;
-    if (!s || !s->ok) continue;
-    *launches += __atomic_load_n(&s->box->launches, __ATOMIC_ACQUIRE);
-    *served += __atomic_load_n(&s->box->served, __ATOMIC_ACQUIRE);
-    *alive += __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE);
-  }
+  for (int kind = 0; kind < 2; kind++)
+    for (int w = 0; w < kSvcWavesMax; w++) {
+      const size_t at = svc_index(device, kind, w);
+      const Service* s = at < v.size() ? v[at] : nullptr;
+      if (!s || !s->ok) continue;
+      *launches += __atomic_load_n(&s->box->launches, __ATOMIC_ACQUIRE);
+      *served += __atomic_load_n(&s->box->served, __ATOMIC_ACQUIRE);
+      *alive += __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE);
+    }
   return KDB_LZ4_OK;
 }
 
