@@ -130,18 +130,25 @@ struct Table12 {
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
     const uint32_t sl = (h & 3u) << 3;
     s.sh = (h & 7u) << 2;
-    s.lo = h;
-    s.hi = (h >> 1) & ~3u;
-    const uint32_t ml = on ? 0xffu << sl : 0u;
-    s.mh = on ? 15u << s.sh : 0u;
+    // A lane whose exchange is off addresses LDS past the kernel's allocation
+    // (reads return 0, writes are dropped: it neither gets nor puts, and its
+    // restore is dropped too) instead of carrying a zero mask and zero data:
+    // one select for the address instead of four on the masks and data
+    // (compress 9.07 -> 9.00 ms, profiles/r04_d/r04_e_ab_exchange_oor.txt)
+    const uint32_t oor = on ? 0u : 0x10000u;
+    s.lo = h | oor;
+    s.hi = ((h >> 1) & ~3u) | oor;
+    const uint32_t ml = 0xffu << sl;
+    s.mh = 15u << s.sh;
+    const uint32_t dl = (p & 0xffu) << sl, dh = ((p >> 8) & 15u) << s.sh;
+    const uint32_t al = (h & ~3u) | oor;
     uint32_t ol, oh;
     asm volatile(
         "ds_mskor_rtn_b32 %0, %2, %3, %4 offset:" KDB_STR(KDB_T12_LO) "\n\t"
         "ds_mskor_rtn_b32 %1, %5, %6, %7 offset:" KDB_STR(KDB_T12_HI) "\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(ol), "=&v"(oh)
-        : "v"(h & ~3u), "v"(ml), "v"(((p & 0xffu) << sl) & ml), "v"(s.hi), "v"(s.mh),
-          "v"((((p >> 8) & 15u) << s.sh) & s.mh)
+        : "v"(al), "v"(ml), "v"(dl), "v"(s.hi), "v"(s.mh), "v"(dh)
         : "memory");
 #if KDB_ABL_DUP_XCHG
     // attribution build (tools/gpurun/lds_attr.sh): the same two exchanges
@@ -172,9 +179,12 @@ struct Table16 {
   __device__ Table16(uint16_t* p) : off(lds_off(p)) {}
   __device__ Table16() : off(0) {}
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
-    s.h = h;
-    const uint32_t sh = (h & 1u) << 4, m = on ? 0xffffu << sh : 0u;
-    const uint32_t o = mskor_rtn(off + ((h & ~1u) << 1), m, ((p & 0xffffu) << sh) & m);
+    // an off lane addresses past the allocation (see Table12::xchg): mixed
+    // batch compress 5.510 -> 5.494 ms (profiles/r04_d/r04_f_ab_exchange_oor16.txt)
+    const uint32_t oor = on ? 0u : 0x8000u;
+    s.h = h | oor;
+    const uint32_t sh = (h & 1u) << 4;
+    const uint32_t o = mskor_rtn(off + ((s.h & ~1u) << 1), 0xffffu << sh, (p & 0xffffu) << sh);
     return (o >> sh) & 0xffffu;
   }
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const {
@@ -189,8 +199,8 @@ struct Table32 {
   __device__ Table32(uint32_t* p) : off(lds_off(p)) {}
   __device__ Table32() : off(0) {}
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
-    s.h = h;
-    return mskor_rtn(off + (h << 2), on ? 0xffffffffu : 0u, on ? p : 0u);
+    s.h = h | (on ? 0u : 0x4000u);      // an off lane: past the allocation (see Table12::xchg)
+    return mskor_rtn(off + (s.h << 2), 0xffffffffu, p);
   }
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const { ((lds_u32*)(uintptr_t)off)[s.h] = v; }
 };
