@@ -145,7 +145,7 @@ __host__ __device__ __forceinline__ uint32_t compress_bound(uint32_t n) {
 __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* lds, uint32_t b) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds);
   uint32_t q = b >> 2;
-  return __builtin_amdgcn_alignbyte(w[q + 1], w[q], b & 3u);
+  return __builtin_amdgcn_alignbyte(w[q + 1], w[q], b & 3u);   // (without the & 3: compress slower, r04_h)
 }
 
 // Copies n bytes at global g (any alignment) into the 16B-aligned LDS buffer
