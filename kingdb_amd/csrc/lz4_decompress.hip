@@ -597,7 +597,7 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
       auto header = [&](uint32_t tq, int tip) {
         const int ln = (int)(tq & 0xffu) >> 4, b1 = (int)((tq >> 8) & 0xffu);
         lx = (ln + 1) >> 4;
-        xl = b1 & -lx;
+        xl = (int)((uint32_t)b1 * (uint32_t)lx);   // lx is 0 or 1 (as in decode_block)
         lit = ln + xl;
         ls = tip + 1 + lx;
       };
@@ -611,7 +611,7 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
         const int e = (int)readlane(v, (l3 + 2u) & 63u);
         const int off = (int)(readlane(v, l3) | (readlane(v, (l3 + 1u) & 63u) << 8));
         const int mx = (mn + 1) >> 4;
-        const int xm = e & -mx;
+        const int xm = e * mx;
         const int mlen = mn + xm + (int)kMinMatch;
         if (unii((lim_ip - vip) | (far_op - vop) | (45 - xl) | (opl - off) | (254 - xm) | ((int)kORing - off)) < 0)
           break;
