@@ -10,17 +10,20 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "lz4_device.h"
+
 namespace kdb_lz4 {
 
 namespace {
-// Per-device pool of 512-byte counter slots (a WorkQueue's 8 counters, 64 B
-// apart).  A launch takes the next slot round-robin and zeroes it on its own
-// stream.  Each slot carries an event recorded on the stream of its last user
-// (work_counter_release, after the launches that read it): a slot handed out
-// again -- 2048 launches later -- first waits for that event, so a slot is
-// never zeroed under a kernel still dequeuing from it, whatever the number of
-// streams and host threads.
-constexpr uint32_t kSlots = 2048, kSlotBytes = 512;
+// Per-device pool of 8 KiB counter slots (a WorkQueue's kQueues counters,
+// kQueueStride apart).  A launch takes the next slot round-robin and zeroes
+// it on its own stream.  Each slot carries an event recorded on the stream of
+// its last user (work_counter_release, after the launches that read it): a
+// slot handed out again -- 1024 launches later -- first waits for that event,
+// so a slot is never zeroed under a kernel still dequeuing from it, whatever
+// the number of streams and host threads.
+constexpr uint32_t kSlotBytes = kQueues * kQueueStride * 4u, kSlots = 1024;
+static_assert(kSlotBytes == 8192u, "32 counters 256 B apart");
 struct Pool {
   uint8_t* base = nullptr;
   std::atomic<uint32_t> next{0};
@@ -224,12 +227,13 @@ hipError_t fork_end(hipStream_t st, hipStream_t aux) {
 // Ranges per launch.  Tiny values saturate one counter (128 Ki 100-byte
 // values: ~70 claims/us), and even at 4 KiB, where the rate is far below
 // that, a contended counter's latency shows: decompress 5.79 ms with one
-// range vs 5.30 ms with eight (1 Mi x 4 KiB).  So: eight, unless overridden.
+// range vs 5.30 ms with eight (1 Mi x 4 KiB), 2.65 ms with kQueues (32, see
+// lz4_device.h) in round 4.  So: kQueues, unless overridden.
 uint32_t work_queues(uint32_t max_len) {
   (void)max_len;
-  static const int env = (int)kdb_tune("KDB_LZ4_QUEUES", 0);   // force 1 or 8 ranges
+  static const int env = (int)kdb_tune("KDB_LZ4_QUEUES", 0);   // force 1 range (or kQueues)
   if (env > 0) return (uint32_t)env;
-  return 8u;   // kQueues (lz4_device.h)
+  return kQueues;
 }
 
 // Values per counter claim: ~1/8 of a workgroup's share, at most 16, so the

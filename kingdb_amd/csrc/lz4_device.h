@@ -77,11 +77,21 @@ __device__ __forceinline__ int leading_zeros_or_neg(uint64_t m) {
 // consecutive value indices with one device-scope atomic.  A single counter
 // saturates near 88 claims/us (microarch "dequeue") -- a launch of 128 Ki
 // 100-byte values was bound by exactly that -- so the index space is split
-// into kQueues ranges with a counter each (64 bytes apart): a workgroup starts
-// on range blockIdx % kQueues and moves to the next range when its own is
-// exhausted (a plain load first, so finished ranges cost no atomics).
-// next() hands out values one ahead of their use.
-constexpr uint32_t kQueues = 8, kQueueStride = 16;   // counters: 8 x u32, 64 B apart (work_counter slots)
+// into kQueues ranges with a counter each: a workgroup starts on range
+// blockIdx % kQueues and moves to the next range when its own is exhausted (a
+// plain load first, so finished ranges cost no atomics).  next() hands out
+// values one ahead of their use.
+//
+// 32 ranges, counters 256 bytes apart.  Eight counters 64 bytes apart still
+// bound the tiny classes: their claims all served together near 60-70 per us
+// (1 Mi x 100 B decompress 1.10 ms, compress 1.02 ms); 32 counters 256 B apart
+// 0.46 / 0.81 ms, the headline decompress 2.81 -> 2.65 ms and the mixed batch's
+// 2.75 -> 2.38 ms (profiles/r04_d/r04_vw_ab_queues.txt: 8 at 4 KiB, 64 at
+// 1 KiB or 4 KiB measured the same as 32 at 256 B).
+#ifndef KDB_GUIDED
+#define KDB_GUIDED 1
+#endif
+constexpr uint32_t kQueues = 32, kQueueStride = 64;   // counters: 32 x u32, 256 B apart (work_counter slots)
 struct WorkQueue {
   uint32_t* ctr;
   uint32_t n, batch, cur, end, nr, q, left;
@@ -97,15 +107,28 @@ struct WorkQueue {
   __device__ __forceinline__ void claim() {
     while (left) {
       const uint32_t lo = (uint32_t)((uint64_t)n * q / nr), hi = (uint32_t)((uint64_t)n * (q + 1u) / nr);
-      uint32_t v = 0;
+      uint32_t v = 0, b = batch;
       if (lane_id() == 0) {
         uint32_t* c = ctr + kQueueStride * q;
-        v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < hi - lo ? atomicAdd(c, batch) : hi - lo;
+        const uint32_t seen = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (seen < hi - lo) {
+#if KDB_GUIDED
+          // guided: claims shrink as the range runs out -- at most 1/4 of
+          // what is left per wave of the range -- so the waves' last claims
+          // end close together (the launch's tail is one small claim)
+          const uint32_t per = (hi - lo - seen) / (4u * max(gridDim.x / nr, 1u));
+          b = per < 1u ? 1u : per < batch ? per : batch;
+#endif
+          v = atomicAdd(c, b);
+        } else {
+          v = hi - lo;
+        }
       }
       v = uni(v);
+      b = uni(b);
       if (v < hi - lo) {
         cur = lo + v;
-        end = min(cur + batch, hi);
+        end = min(cur + b, hi);
         return;
       }
       q = q + 1u == nr ? 0u : q + 1u;
