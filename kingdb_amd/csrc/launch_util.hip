@@ -236,6 +236,12 @@ uint32_t work_queues(uint32_t max_len) {
   return kQueues;
 }
 
+uint32_t claim_guide(uint32_t max_len) {
+  static const long env = kdb_tune("KDB_LZ4_GUIDE", -1);   // force a guide (0 = off)
+  if (env >= 0) return (uint32_t)env;
+  return max_len >= 2048u ? 4u : 0u;
+}
+
 // Values per counter claim: ~1/8 of a workgroup's share, at most 16, so the
 // claim rate stays far below one counter's ceiling and the tail stays short.
 uint32_t claim_batch(uint32_t n, uint32_t grid) {

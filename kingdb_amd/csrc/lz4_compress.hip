@@ -727,7 +727,7 @@ __device__ __forceinline__ void values_loop(
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
-    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, uint32_t nq) {
+    int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, uint32_t nq, uint32_t guide) {
   const uint32_t lane = lane_id();
   uint16_t* tab16 = reinterpret_cast<uint16_t*>(smem);
   constexpr uint32_t kTabBytes = kSmall ? kTable12Bytes : kTableBytes;
@@ -747,7 +747,7 @@ __device__ __forceinline__ void values_loop(
   // register prefetch (kSmall): the next value's realigned 16-byte chunks
   uint4 pa[kPrefetch], pb[kPrefetch];
   uint32_t p_head = 0, p_chunks = 0;
-  WorkQueue wq = WorkQueue::make(work, n, batch, nq);
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide);
   uint32_t v = uni(wq.next());
   auto prefetch = [&](uint32_t w) {
     if (w < n) {
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ dst_cap, uint32_t* __restrict__ frame_len,
     int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch, const uint32_t* __restrict__ census,
-    uint32_t cls, uint32_t nq) {
+    uint32_t cls, uint32_t nq, uint32_t guide) {
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
   // kSmall: a fixed LDS layout at LDS address 0 (the kernel's only LDS
   // array), so every LDS address is a constant offset (a dynamic
@@ -847,7 +847,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
   values_loop<kFrame, kSmall>(kSmall ? smem_s : smem_d, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
-                              dst_cap, frame_len, ret, work, batch, nq);
+                              dst_cap, frame_len, ret, work, batch, nq, guide);
 }
 
 // ---------------------------------------------------------------------------
@@ -1072,7 +1072,7 @@ __global__ __launch_bounds__(64) void lz4_compress_mixed_kernel(
                             ret, work_big, batch_big);
   __syncthreads();
   values_loop<kFrame, true>(reinterpret_cast<uint8_t*>(smem32), src, src_off, src_len, n, 0u, kSmallMax, dst,
-                            dst_off, dst_cap, frame_len, ret, work_small, batch_small, nq);
+                            dst_off, dst_cap, frame_len, ret, work_small, batch_small, nq, 0u);
 }
 
 // Values per size class (len <= b0, <= b1, <= b2, above), so that a class
@@ -1096,7 +1096,8 @@ template <bool F, bool Sm>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
-                             int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0) {
+                             int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0,
+                             uint32_t guide = 0) {
   auto kern = lz4_compress_kernel<F, Sm>;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t* work = nullptr;
@@ -1106,7 +1107,7 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   launch_note(F ? (Sm ? "lz4_compress_kernel<true, true>" : "lz4_compress_kernel<true, false>")
                 : (Sm ? "lz4_compress_kernel<false, true>" : "lz4_compress_kernel<false, false>"));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
-                     dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap));
+                     dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap), guide);
   e = hipGetLastError();
   const hipError_t r = work_counter_release(st, work);   // the slot is fenced even when the launch failed
   return e != hipSuccess ? e : r;
@@ -1222,10 +1223,11 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     }
     if (on[0] && !combo) {
       const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
+      const uint32_t guide = claim_guide(min(max_len, kSmallMax));
       r = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                         frame_len, ret, census, 0)
+                                         frame_len, ret, census, 0, guide)
                 : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                          frame_len, ret, census, 0);
+                                          frame_len, ret, census, 0, guide);
       if (r != hipSuccess) return r;
     }
     // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
@@ -1235,9 +1237,9 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
       const uint32_t top = min(max_len, hi[1]);
       const size_t lds = compress_lds_bytes(top);
       r = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
-                                          dst_cap, frame_len, ret, census, 1)
+                                          dst_cap, frame_len, ret, census, 1, claim_guide(top))
                 : launch_one<false, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
-                                           dst_cap, frame_len, ret, census, 1);
+                                           dst_cap, frame_len, ret, census, 1, claim_guide(top));
     }
     return r;
   };

@@ -88,21 +88,25 @@ __device__ __forceinline__ int leading_zeros_or_neg(uint64_t m) {
 // 0.46 / 0.81 ms, the headline decompress 2.81 -> 2.65 ms and the mixed batch's
 // 2.75 -> 2.38 ms (profiles/r04_d/r04_vw_ab_queues.txt: 8 at 4 KiB, 64 at
 // 1 KiB or 4 KiB measured the same as 32 at 256 B).
-#ifndef KDB_GUIDED
-#define KDB_GUIDED 1
-#endif
 constexpr uint32_t kQueues = 32, kQueueStride = 64;   // counters: 32 x u32, 256 B apart (work_counter slots)
 struct WorkQueue {
   uint32_t* ctr;
-  uint32_t n, batch, cur, end, nr, q, left;
+  uint32_t n, batch, cur, end, nr, q, left, guide;
   // nr ranges: 1, or kQueues for launches whose claim rate would saturate one
   // counter (work_queues() on the host picks)
   // c == nullptr: a direct launch (grid == n, see launch_counter), workgroup b
   // takes value b and nothing else -- no counter, so no memset before it.
-  __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr) {
-    if (!c) return WorkQueue{c, n, batch, blockIdx.x, min(blockIdx.x + 1u, n), 1u, 0u, 0u};
+  // guide > 0: guided claims -- a claim takes at most 1/guide of what is left
+  // per wave of its range, so claims shrink as a range runs out and the waves'
+  // last claims end close together (the launch's tail is one small claim).
+  // For values with work enough per claim (the host sets it from the batch's
+  // largest value): 1 Mi x 4 KiB compress 9.01 -> 8.85 ms; 100-byte values
+  // and the decoders lose more to the extra claims than the tail gives back
+  // (profiles/r04_d/r04_y_ab_guided.txt).
+  __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr, uint32_t guide = 0) {
+    if (!c) return WorkQueue{c, n, batch, blockIdx.x, min(blockIdx.x + 1u, n), 1u, 0u, 0u, 0u};
     nr = nr > 1u ? kQueues : 1u;
-    return WorkQueue{c, n, batch, 0u, 0u, nr, (uint32_t)blockIdx.x % nr, nr};
+    return WorkQueue{c, n, batch, 0u, 0u, nr, (uint32_t)blockIdx.x % nr, nr, guide};
   }
   __device__ __forceinline__ void claim() {
     while (left) {
@@ -112,13 +116,10 @@ struct WorkQueue {
         uint32_t* c = ctr + kQueueStride * q;
         const uint32_t seen = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (seen < hi - lo) {
-#if KDB_GUIDED
-          // guided: claims shrink as the range runs out -- at most 1/4 of
-          // what is left per wave of the range -- so the waves' last claims
-          // end close together (the launch's tail is one small claim)
-          const uint32_t per = (hi - lo - seen) / (4u * max(gridDim.x / nr, 1u));
-          b = per < 1u ? 1u : per < batch ? per : batch;
-#endif
+          if (guide) {
+            const uint32_t per = (hi - lo - seen) / (guide * max(gridDim.x / nr, 1u));
+            b = per < 1u ? 1u : per < batch ? per : batch;
+          }
           v = atomicAdd(c, b);
         } else {
           v = hi - lo;
@@ -230,6 +231,8 @@ uint32_t services_resident(int dev);
 // the scalar entry points' latency); otherwise a zeroed counter slot.
 hipError_t launch_counter(hipStream_t st, uint32_t n, uint32_t grid, uint32_t** ctr);
 uint32_t claim_batch(uint32_t n, uint32_t grid);
+// the WorkQueue guide for a launch whose values are up to max_len bytes
+uint32_t claim_guide(uint32_t max_len);
 // WorkQueue ranges for a launch whose values are at most max_len bytes
 uint32_t work_queues(uint32_t max_len);
 // size-class launches on a second stream: *aux waits for st's work so far;
