@@ -1084,11 +1084,22 @@ __global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n
     const uint32_t L = len[v];
     c[L <= b0 ? 0 : L <= b1 ? 1 : L <= b2 ? 2 : 3]++;
   }
+  // per block: the waves' sums in LDS, then one atomic per class (one per
+  // wave and class, on a grid of 1 024 blocks -- 16 Ki same-address atomics
+  // for 1 Mi values -- took 92 us of a mixed batch's compress step)
+  __shared__ uint32_t part[4][4];
+  const uint32_t w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     uint32_t x = c[k];
     for (int d = 32; d >= 1; d >>= 1) x += (uint32_t)__shfl_xor((int)x, d);
-    if (lane_id() == 0 && x) atomicAdd(&counts[k], x);
+    if (lane_id() == 0) part[w][k] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4u) {
+    uint32_t x = 0;
+    for (uint32_t i = 0; i < (blockDim.x >> 6); ++i) x += part[i][threadIdx.x];
+    if (x) atomicAdd(&counts[threadIdx.x], x);
   }
 }
 
@@ -1186,7 +1197,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   if (classes > 1) {
     e = work_counter(st, &census);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(class_census_kernel, dim3(min((n + 255u) / 256u, 1024u)), dim3(256), 0, st, src_len, n,
+    hipLaunchKernelGGL(class_census_kernel, dim3(min((n + 255u) / 256u, 256u)), dim3(256), 0, st, src_len, n,
                        kSmallMax, b1, k64KLimit - 1u, census);
   }
   // The in-place classes (8 KiB .. 65 546 B, and byU32) go first, on a
@@ -1194,7 +1205,8 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   // and the small classes fill the GPU around their tail.  With both the
   // small and the byU16 in-place class, one launch takes both
   // (lz4_compress_mixed_kernel: in-place values first, then the small ones).
-  const bool combo = on[0] && on[2];
+  static const bool combo_on = kdb_tune("KDB_LZ4_CMIXED", 1) != 0;   // 0: separate class launches (A/B)
+  const bool combo = combo_on && on[0] && on[2];
   hipStream_t aux = st;
   const bool fork = combo ? on[3] : ((on[2] || on[3]) && (on[0] || on[1]));
   // The class launches stop at the first error, but the join of the forked

@@ -9,6 +9,6 @@ for kv in "$@"; do
   if [ "$kv" = "-" ]; then
     timeout -k 10 150 python tools/ab.py kingdb_amd/var/var_$v.so "${args[@]}" >> gpurun_out/${tag}.txt 2>&1 || exit 1
   else
-    env "$kv" timeout -k 10 150 python tools/ab.py kingdb_amd/var/var_$v.so "${args[@]}" >> gpurun_out/${tag}.txt 2>&1 || exit 1
+    env $kv timeout -k 10 150 python tools/ab.py kingdb_amd/var/var_$v.so "${args[@]}" >> gpurun_out/${tag}.txt 2>&1 || exit 1
   fi
 done
