@@ -744,8 +744,13 @@ __device__ __forceinline__ void values_loop(
     for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(s_tab)[i] = z4;
   }
 
-  // register prefetch (kSmall): the next value's realigned 16-byte chunks
-  uint4 pa[kPrefetch], pb[kPrefetch];
+  // register prefetch (kSmall): the next value's realigned 16-byte chunks.
+  // (Round 4 tried waiting for them with an explicit vmcnt that leaves the
+  // value's last 16 byte stores in flight -- loads into accumulation
+  // registers the compiler does not track: digest-identical and no faster,
+  // 8.80 -> 8.83 ms, profiles/r04_d/r04_n_ab_counted_wait.txt.)
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 pa[kPrefetch], pb[kPrefetch];
   uint32_t p_head = 0, p_chunks = 0;
   WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide);
   uint32_t v = uni(wq.next());
@@ -764,8 +769,9 @@ __device__ __forceinline__ void values_loop(
 #pragma unroll
         for (uint32_t i = 0; i < kPrefetch; ++i) {
           const uint32_t c = lane + 64u * i;
-          pa[i] = base[min(c, last)];
-          pb[i] = base[min(c + 1u, last)];
+          const uint4 a = base[min(c, last)], b = base[min(c + 1u, last)];
+          pa[i] = u32x4{a.x, a.y, a.z, a.w};
+          pb[i] = u32x4{b.x, b.y, b.z, b.w};
         }
       }
     }
@@ -777,19 +783,30 @@ __device__ __forceinline__ void values_loop(
     const uint32_t S = sload(src_len, v);
     const uint8_t* g = src + sload(src_off, v);
     uint8_t* o = dst + sload(dst_off, v);
-    if (S < min_len || S > in_cap) {             // another size class's launch owns it
-      if (kSmall) prefetch(vn);
+    const bool mine = S >= min_len && S <= in_cap;   // else another size class's launch owns it
+    if (kSmall) {
+      // staging, then the next value's prefetch at ONE place on every path:
+      // with two prefetch sites the compiler joined their registers with
+      // copies at the loop's latch, and a copy of a register a load is
+      // still filling waits for it -- and, vmcnt being in order, for every
+      // byte store of the value just compressed
+      if (mine) {
+#pragma unroll
+        for (uint32_t i = 0; i < kPrefetch; ++i) {
+          const uint32_t c = lane + 64u * i;
+          if (c < p_chunks)
+            reinterpret_cast<uint4*>(s_in)[c] =
+                funnel16(make_uint4(pa[i].x, pa[i].y, pa[i].z, pa[i].w), make_uint4(pb[i].x, pb[i].y, pb[i].z, pb[i].w),
+                         p_head);
+        }
+      }
+      prefetch(vn);                  // the next value's loads fly while this one is parsed
+    }
+    if (!mine) {
       v = vn;
       continue;
     }
-    if (kSmall) {
-#pragma unroll
-      for (uint32_t i = 0; i < kPrefetch; ++i) {
-        const uint32_t c = lane + 64u * i;
-        if (c < p_chunks) reinterpret_cast<uint4*>(s_in)[c] = funnel16(pa[i], pb[i], p_head);
-      }
-      prefetch(vn);                  // the next value's loads fly while this one is parsed
-    } else {
+    if (!kSmall) {
       stage_aligned(g, S, s_in);
       for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
     }
