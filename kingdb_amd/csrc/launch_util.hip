@@ -242,6 +242,16 @@ uint32_t claim_guide(uint32_t max_len) {
   return max_len >= 2048u ? 4u : 0u;
 }
 
+// The LDS decoder's launches: guide 1 (a claim at most all that is left per
+// wave of its range) for values >= 2 KiB: 1 Mi x 4 KiB decompress 2.64 ->
+// 2.59 ms (guide 2 the same; profiles/r04_d/r04_q_ab_decode_guide.txt); the
+// 100-byte class keeps fixed claims (a guide cost it more claims than tail).
+uint32_t decode_guide(uint32_t max_out) {
+  static const long env = kdb_tune("KDB_LZ4_DGUIDE", -1);   // force a guide (0 = off)
+  if (env >= 0) return (uint32_t)env;
+  return max_out >= 2048u ? 1u : 0u;
+}
+
 // Values per counter claim: ~1/8 of a workgroup's share, at most 16, so the
 // claim rate stays far below one counter's ceiling and the tail stays short.
 uint32_t claim_batch(uint32_t n, uint32_t grid) {

@@ -368,7 +368,7 @@ __device__ __forceinline__ void small_decode_loop(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t skip_big, uint32_t nq) {
+    uint32_t skip_big, uint32_t nq, uint32_t guide = 0) {
   const uint32_t lane = lane_id();
   // [staged block + 16 zero bytes][output window + 64 bytes of slack for the
   // decoder's unmasked 64-byte steps]; the register window may read 256 bytes
@@ -381,7 +381,7 @@ __device__ __forceinline__ void small_decode_loop(
   uint4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {}, pf4 = {};
   uint32_t pf_head = 0, pf_chunks = 0;
 
-  WorkQueue wq = WorkQueue::make(work, n, batch, nq);
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide);
   uint32_t v = uni(wq.next());
   prefetch_value<kPF>(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, v, n, src, src_off, in_len, s_in_cap);
 #pragma unroll 1
@@ -478,10 +478,10 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t skip_big, uint32_t nq) {
+    uint32_t skip_big, uint32_t nq, uint32_t guide) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   small_decode_loop<kFrame, kPF>(smem, src, src_off, in_len, n, in_cap, out_cap_max, dst, dst_off, out_cap, target,
-                            out_len, ret, work, batch, skip_big, nq);
+                            out_len, ret, work, batch, skip_big, nq, guide);
 }
 
 // ---------------------------------------------------------------------------
@@ -1048,7 +1048,8 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   launch_note(F ? (pf3 ? "lz4_decompress_kernel<true, 3u>" : "lz4_decompress_kernel<true, 5u>")
                 : (pf3 ? "lz4_decompress_kernel<false, 3u>" : "lz4_decompress_kernel<false, 5u>"));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
-                     out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out));
+                     out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out),
+                     decode_guide(max_out));
   e = hipGetLastError();
   const hipError_t r = work_counter_release(st, work);   // the slot is fenced even when the launch failed
   return e != hipSuccess ? e : r;

@@ -233,6 +233,8 @@ hipError_t launch_counter(hipStream_t st, uint32_t n, uint32_t grid, uint32_t** 
 uint32_t claim_batch(uint32_t n, uint32_t grid);
 // the WorkQueue guide for a launch whose values are up to max_len bytes
 uint32_t claim_guide(uint32_t max_len);
+// the same for the LDS decoder's launches (max_out: their largest output)
+uint32_t decode_guide(uint32_t max_out);
 // WorkQueue ranges for a launch whose values are at most max_len bytes
 uint32_t work_queues(uint32_t max_len);
 // size-class launches on a second stream: *aux waits for st's work so far;
