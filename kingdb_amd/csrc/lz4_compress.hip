@@ -367,7 +367,24 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // values only: for byU32 ones (1 MiB parts) it measured slower (8.47 ->
     // 9.01 ms per 600 x 1 MiB).
     constexpr bool kWin = !kFree && !kWide;
+#ifndef KDB_LZ4_SEQ_WINDOW
+#define KDB_LZ4_SEQ_WINDOW 1
+#endif
     uint32_t win = 0, wbase = 0x80000000u, pwin = 0, pbase = 0x80000000u;
+#if KDB_LZ4_SEQ_WINDOW
+    // Round 4 (KDB_LZ4_SEQ_WINDOW, the default; 0 = the round-3 window
+    // above): one 256-byte window per sequence, loaded at the sequence's
+    // start from 64 bytes before its first search position -- an address
+    // known before the search -- so it lands with the candidate words, and
+    // the count's bytes, the literals and the next sequence's input words
+    // come out of it by ds_bpermute whenever they lie in it (near matches:
+    // all of G1's).  The sequence's chain is then one global round trip
+    // (candidate words and window together) instead of two (the candidate
+    // words, then the window's newest line, an HBM miss).  64 KiB x 10 486
+    // compress 3.71 -> 3.37 ms, mixed batch 5.34 -> 5.04 ms
+    // (profiles/r04_d/r04_u_ab_sequence_window.txt, digest-gated).
+    uint32_t sw = 0, sbase = 0x80000000u;
+#endif
     // One sequence per call.  The sequence loop runs while anchor < lim_end:
     // mflimit + 1 (lz4.cc:597: a match that ends past mflimit leaves for the
     // last literals), or 0 once a search finds no match (the last literals)
@@ -420,15 +437,39 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // harmless, clamped into the value only in HBM); the masks are
         // built while they are in flight
         const uint32_t ia = ip - 1u - lane, ra = ref - 1u - lane, ib = ip + kMinMatch + lane;
+#if KDB_LZ4_SEQ_WINDOW
+        uint32_t a0, b0, a1, b1;
+        uint32_t lim_w = lim;
+        const uint32_t iw = ip - sbase, rw = ref - sbase;
+        if (kWin && max(iw, rw) <= 188u) {
+          // the catch-up's ref side has rw bytes before it in the window
+          auto wbyte = [&](uint32_t d) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(d & ~3u), (int)sw);
+            return (w >> ((d & 3u) << 3)) & 0xffu;
+          };
+          a0 = wbyte(iw - 1u - lane);
+          b0 = wbyte(rw - 1u - lane);
+          a1 = wbyte(iw + kMinMatch + lane);
+          b1 = wbyte(rw + kMinMatch + lane);
+          lim_w = min(lim, rw);
+        } else {
+          a0 = src.u8(clamp1(ia));
+          b0 = src.u8(clamp1(ra));
+          a1 = src.u8(clamp1(ib));
+          b1 = src.u8(clamp1(ref + kMinMatch + lane));
+        }
+#else
+        const uint32_t lim_w = lim;
         const uint32_t a0 = src.u8(clamp1(ia)), b0 = src.u8(clamp1(ra));
         const uint32_t a1 = src.u8(clamp1(ib));
         const uint32_t b1 = src.u8(clamp1(ref + kMinMatch + lane));
+#endif
         // in-place values: the restore (table writes) goes out behind the
         // count's reads (value bytes in HBM, no overlap), so their issue does
         // not wait behind it; it lands before the next sequence's exchange
         // all the same (measured: mixed batch compress -2 %; LDS-staged
         // values restore first, below the search: +1.7 % the other way)
-        if constexpr (kWin) {
+        if constexpr (kWin && !KDB_LZ4_SEQ_WINDOW) {
           pwin = win;
           pbase = wbase;
           wbase = ip;
@@ -448,14 +489,14 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // (in-place values, whose reads are clamped, compare the lane with
         // lim and rem: measured a little faster there)
         const uint32_t x0 = kFree ? ((int)ra >= 0 ? ((int)ia >= (int)anchor ? a0 : k256) : k257)
-                                  : (lane < lim ? a0 : k256);
+                                  : (lane < lim_w ? a0 : k256);
         const uint32_t x1 = kFree ? (ib < matchlimit ? a1 : k256) : (lane < rem ? a1 : k256);
         const int c0 = first_zero_or_neg(__builtin_amdgcn_uicmp(x0, b0, 32 /*EQ*/));
         const int ml0 = first_zero_or_neg(__builtin_amdgcn_uicmp(x1, b1, 32 /*EQ*/));
         c = (uint32_t)c0;
         ml = (uint32_t)ml0;
         // one scalar test for the rare continuations of either count
-        if (__builtin_expect((c0 | ml0) < 0, 0)) {
+        if (__builtin_expect((c0 | ml0) < 0 || lim_w < lim, 0)) {
         if (ml0 < 0) {
           ml = 64u;
 #pragma unroll 1
@@ -468,8 +509,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
             if (d < 64u) break;
           }
         }
-        if (c0 < 0) {
-          c = 64u;
+        const uint32_t cs_ = c0 < 0 ? 64u : (uint32_t)c0;
+        c = cs_;
+        if (cs_ < lim && (c0 < 0 || cs_ == lim_w)) {
 #pragma unroll 1
           for (;;) {
             const bool l2 = lane < lim - c;
@@ -556,6 +598,25 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         } else {
           // next input words: bytes ip_end - 2 + lane .. +3, at window offset
           // ml + 2 + lane (ml before the catch-up); covered while ml <= 187
+#if KDB_LZ4_SEQ_WINDOW
+          const uint32_t pw = ip_end - sbase;
+          if (pw <= 190u) {
+            const uint32_t d = pw - 2u + lane;
+            const uint32_t w0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((d >> 2) << 2), (int)sw);
+            const uint32_t w1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((d >> 2) + 1u) << 2), (int)sw);
+            seq0 = typename Src::Word{__builtin_amdgcn_alignbyte(w1, w0, d & 3u)};
+          } else {
+            seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+          }
+          const uint32_t lo = seq_anchor - sbase;
+          if (lo + lit <= 256u) {
+            const uint32_t o = lo + da;
+            const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((o >> 2) << 2), (int)sw);
+            lb = w >> ((o & 3u) << 3);
+          } else {
+            lb = src.u8(clamp1(seq_anchor + da));
+          }
+#else
           const uint32_t mw = ip_end - wbase;               // 4 + ml
           if (mw <= 191u) {
             const uint32_t d = mw - 2u + lane;
@@ -575,6 +636,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           } else {
             lb = src.u8(clamp1(seq_anchor + da));
           }
+#endif
         }
         const uint32_t head = ((min(vlit, kRunMask) << 4) | min(vml, kMlMask)) | (remL << 8);
         const uint32_t tail = moff | (remM << 16);
@@ -601,6 +663,13 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
       // cost more than it saved (64 KiB 6.51 -> 6.36 ms without it; 1 MiB
       // byU32 9.84 -> 10.71 ms without it, profiles/r02_e40_ab_touch.txt)
       if constexpr (kWide) src.step(anchor + 1u);
+#if KDB_LZ4_SEQ_WINDOW
+      if constexpr (kWin) {
+        const uint32_t cs = anchor + 1u - 3u * (decltype(lead_c)::value ? 1u : 0u);   // the first chunk's start
+        sbase = cs >= 64u ? cs - 64u : 0u;
+        sw = src.rd32(min(sbase + 4u * lane, last4));
+      }
+#endif
       // ================= search (lz4.cc:494-527), 64 iterations per step
       // (the loop exits with the chunk that matched; a chunk that runs past
       // mflimit without a match goes to the last literals)
