@@ -370,7 +370,9 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
 #ifndef KDB_LZ4_SEQ_WINDOW
 #define KDB_LZ4_SEQ_WINDOW 1
 #endif
+#if !KDB_LZ4_SEQ_WINDOW
     uint32_t win = 0, wbase = 0x80000000u, pwin = 0, pbase = 0x80000000u;
+#endif
 #if KDB_LZ4_SEQ_WINDOW
     // Round 4 (KDB_LZ4_SEQ_WINDOW, the default; 0 = the round-3 window
     // above): one 256-byte window per sequence, loaded at the sequence's
@@ -469,12 +471,14 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // not wait behind it; it lands before the next sequence's exchange
         // all the same (measured: mixed batch compress -2 %; LDS-staged
         // values restore first, below the search: +1.7 % the other way)
-        if constexpr (kWin && !KDB_LZ4_SEQ_WINDOW) {
+#if !KDB_LZ4_SEQ_WINDOW
+        if constexpr (kWin) {
           pwin = win;
           pbase = wbase;
           wbase = ip;
           win = src.rd32(min(ip + 4u * lane, last4));
         }
+#endif
         if constexpr (!kFree) {
           if (ip - refk < pk - refk) tab.restore(slot, refk);
         }
