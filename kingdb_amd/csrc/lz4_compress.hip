@@ -1273,7 +1273,10 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
   hipError_t e = lane_order_ok();
   if (e != hipSuccess) return e;
   static const uint32_t mid_split = (uint32_t)kdb_tune("KDB_LZ4_CSPLIT", kMidLdsMax);
-  const uint32_t b1 = min(max(mid_split, kSmallMax), k64KLimit - 1u);   // top of the LDS-staged class
+  // top of the LDS-staged class; at most 48 KiB: Table16's off lanes address
+  // 64 KiB past the table, which must lie past the staged value too (a
+  // tuning split of 65 546 measured wrong frames, profiles/r04_d/r04_cs_*)
+  const uint32_t b1 = min(max(mid_split, kSmallMax), min(k64KLimit - 1u, 65536u - kTableBytes));
   // class c covers lengths [lo[c], hi[c]]
   const uint32_t lo[4] = {0u, kSmallMax + 1u, b1 + 1u, k64KLimit};
   const uint32_t hi[4] = {kSmallMax, b1, k64KLimit - 1u, 0xFFFFFFFFu};

@@ -495,11 +495,20 @@ __global__ __launch_bounds__(64) void lz4_decompress_kernel(
 //     past the block end staged as 0, like the zeroed tail of the LDS decoder),
 //     plus a 512-byte mirror of its start so the 256-byte register window
 //     never wraps.
-constexpr uint32_t kIRing = 8192u, kIMask = kIRing - 1u, kIHalf = 4096u, kIMirror = 512u;
-template <uint32_t kORing>
-constexpr size_t ring_lds() { return kORing + kIRing + kIMirror; }
+// The input ring's size is kIR: 8 KiB (refilled 4 KiB at a time) where few
+// values run at once (1 MiB parts), 4 KiB in the mixed launch when every
+// value fits byU16 (<= 65 546 bytes): 8.7 KiB of LDS per wave instead of
+// 12.8, 18 waves per CU instead of 12 (64 KiB values 1.33 -> 1.07 ms;
+// 1 MiB parts 4.71 -> 4.80 ms with it, so they keep 8 KiB;
+// profiles/r04_d/r04_ir_ab_input_ring.txt).
+constexpr uint32_t kIMirror = 512u;
+template <uint32_t kORing, uint32_t kIR>
+constexpr size_t ring_lds() { return kORing + kIR + kIMirror; }
 
+template <uint32_t kIR>
 struct InRing {
+  static constexpr uint32_t kIRing = kIR, kIMask = kIR - 1u, kIHalf = kIR / 2u;
+  static_assert(kIHalf >= kIMirror && (kIR & kIMask) == 0u, "a power-of-two ring of two halves, each >= the mirror");
   uint8_t* lds;          // kIRing + kIMirror bytes
   const uint8_t* g;      // block start in HBM
   uint32_t csize;
@@ -539,6 +548,7 @@ struct InRing {
 };
 
 // 256-byte register window over the input ring (ring coordinates).
+template <uint32_t kIMask>
 struct RingWindow {
   const uint32_t* w32;
   uint32_t base, win;
@@ -555,16 +565,17 @@ struct RingWindow {
   }
 };
 
-template <uint32_t kORing>
-__device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __restrict__ o, int csize, int osize,
+template <uint32_t kORing, uint32_t kIR>
+__device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t* __restrict__ o, int csize, int osize,
                            int target) {
   constexpr uint32_t kOMask = kORing - 1u;
+  constexpr uint32_t kIRing = kIR, kIMask = kIR - 1u;
   const uint32_t lane = lane_id();
   const int iend = unii(csize), oend = unii(osize);
   const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
   const int far_ip = iend - (int)(2 + 1 + kLastLiterals) - 62;   // as in decode_block
   const int far_op = min(oexit - 60, oend - (int)kLastLiterals - 60 - 273);
-  RingWindow wd{reinterpret_cast<const uint32_t*>(in.lds), 0u, 0u};
+  RingWindow<kIMask> wd{reinterpret_cast<const uint32_t*>(in.lds), 0u, 0u};
   wd.invalidate();
   in.ensure(kIRing);
   if (osize == 0) return (csize == 1 && (wd.get4(0) & 0xffu) == 0) ? 0 : -1;   // lz4.cc:911
@@ -798,7 +809,7 @@ __device__ int decode_ring(InRing& in, uint8_t* __restrict__ ring, uint8_t* __re
 }
 
 // Values of this launch's class: out size > out_small or block > in_small.
-template <bool kFrame, uint32_t kORing>
+template <bool kFrame, uint32_t kORing, uint32_t kIR>
 __device__ __forceinline__ void ring_decode_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
@@ -881,8 +892,8 @@ __device__ __forceinline__ void ring_decode_loop(
           continue;
         }
       }
-      InRing in{iring, g, (uint32_t)csize, 0u};
-      const int r = decode_ring<kORing>(in, ring, o, csize, osize, tgt);
+      InRing<kIR> in{iring, g, (uint32_t)csize, 0u};
+      const int r = decode_ring<kORing, kIR>(in, ring, o, csize, osize, tgt);
       if (lane == 0) {
         if (kFrame) {
           ret[v] = r > 0 ? 0 : -1;
@@ -906,7 +917,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
     uint32_t prio) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   if (prio) __builtin_amdgcn_s_setprio(2);     // a mixed batch's critical path (see launch_compress)
-  ring_decode_loop<kFrame, kORing>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+  ring_decode_loop<kFrame, kORing, 8192u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
                                    out_len, ret, work, batch);
 }
 
@@ -917,7 +928,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
 // sizes so the staged block and window fit the same LDS), so the small values
 // fill the tail of the long ones instead of splitting the CUs with them from
 // the start (lz4_compress_mixed_kernel does the same on the write side).
-template <bool kFrame>
+template <bool kFrame, uint32_t kIR>
 __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
@@ -926,7 +937,7 @@ __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work_big, uint32_t batch_big,
     uint32_t* __restrict__ work_small, uint32_t batch_small, uint32_t nq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  ring_decode_loop<kFrame, 4096u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+  ring_decode_loop<kFrame, 4096u, kIR>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
                                   out_len, ret, work_big, batch_big);
   __syncthreads();
   small_decode_loop<kFrame, 5u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
@@ -1061,7 +1072,7 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                              const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   auto kern = lz4_decompress_big_kernel<F, R>;
   static const uint32_t prio = env_prio();
-  const size_t lds = ring_lds<R>();
+  const size_t lds = ring_lds<R, 8192u>();
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t* work = nullptr;
   hipError_t e = launch_counter(st, n, grid, &work);
@@ -1102,13 +1113,14 @@ static hipError_t launch_ring(hipStream_t st, const uint8_t* src, const uint64_t
   }
 }
 
-template <bool F>
+template <bool F, uint32_t kIR>
 static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
                                uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst,
                                const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
                                uint32_t* out_len, int32_t* ret) {
-  auto kern = lz4_decompress_mixed_kernel<F>;
-  const size_t lds = ring_lds<4096u>();
+  auto kern = lz4_decompress_mixed_kernel<F, kIR>;
+  const size_t lds = ring_lds<4096u, kIR>();
+  if (decompress_lds_bytes(in_small, out_small) > lds) return hipErrorInvalidValue;   // the small pass's staging
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t *wb = nullptr, *ws = nullptr;
   hipError_t e = launch_counter(st, n, grid, &wb);
@@ -1128,8 +1140,11 @@ static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_
 // of that, plus a frame header); the ring decoder after it for the rest.
 constexpr uint32_t kOutSmallMax = k64KLimit - 1u;
 // the LDS decoder's limit inside lz4_decompress_mixed_kernel: its staged block
-// and window (decompress_lds_bytes) fit the ring decoder's LDS
-constexpr uint32_t kMixedOutSmall = 6144u;
+// and window (decompress_lds_bytes) fit the ring decoder's LDS -- 12.8 KiB with
+// the 8 KiB input ring, 8.7 KiB with the 4 KiB one
+constexpr uint32_t kMixedOutSmall8 = 6144u, kMixedOutSmall4 = 4096u;
+static_assert(kMixedOutSmall4 + kMixedOutSmall4 / 255u + 24u + 32u + 15u + kMixedOutSmall4 + 64u <= 4096u + 4096u + kIMirror,
+              "the small pass's staging fits the 4 KiB input ring's LDS");
 
 hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
   const size_t lds = decompress_lds_bytes(kSvcMaxIn, kSvcMaxOut);
@@ -1160,12 +1175,19 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
   // limit lowered so that its staging fits the ring decoder's LDS
   static const bool combo_on = kdb_tune("KDB_LZ4_DMIXED", 1) != 0;
   if (big && !ring_only && combo_on) {
-    const uint32_t mo2 = min(mo, kMixedOutSmall);
-    const uint32_t mi2 = min(mi, kMixedOutSmall + kMixedOutSmall / 255u + 16u + 8u);
-    return frame ? launch_mixed<true>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target, out_len,
-                                      ret)
-                 : launch_mixed<false>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target, out_len,
-                                       ret);
+    // values whose output fits byU16 only: the 4 KiB input ring (see InRing)
+    if (max_out <= kOutSmallMax) {
+      const uint32_t mo2 = min(mo, kMixedOutSmall4), mi2 = min(mi, kMixedOutSmall4 + kMixedOutSmall4 / 255u + 16u + 8u);
+      return frame ? launch_mixed<true, 4096u>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target,
+                                               out_len, ret)
+                   : launch_mixed<false, 4096u>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target,
+                                                out_len, ret);
+    }
+    const uint32_t mo2 = min(mo, kMixedOutSmall8), mi2 = min(mi, kMixedOutSmall8 + kMixedOutSmall8 / 255u + 16u + 8u);
+    return frame ? launch_mixed<true, 8192u>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target,
+                                             out_len, ret)
+                 : launch_mixed<false, 8192u>(st, src, src_off, in_len, n, mi2, mo2, dst, dst_off, out_cap, target,
+                                              out_len, ret);
   }
   if (ring_only)
     return frame ? launch_ring<true>(st, src, src_off, in_len, n, mi, mo, dst, dst_off, out_cap, target, out_len, ret)
