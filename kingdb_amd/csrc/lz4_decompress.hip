@@ -809,32 +809,49 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
 }
 
 // Values of this launch's class: out size > out_small or block > in_small.
-template <bool kFrame, uint32_t kORing, uint32_t kIR>
+template <bool kFrame, uint32_t kORing, uint32_t kIR, bool kWQ>
 __device__ __forceinline__ void ring_decode_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_small, uint32_t out_small,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
-    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
+    uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    uint32_t nq) {
   const uint32_t lane = lane_id();
   uint8_t* ring = smem;
   uint8_t* iring = smem + kORing;
+  // kWQ: claims of up to `batch` values from the launch's work queues -- a
+  // mixed batch's ring pass scans every index (65 536 claims for 1 Mi
+  // values), which one counter serves at ~65 claims/us: mixed decompress
+  // 2.29 -> 2.00 ms.  Else one counter: the queues' state, live across the
+  // decode, cost 3 % on 1 MiB parts (and 2-8 % in the in-place compressor,
+  // which keeps its one counter; profiles/r04_d/r04_wq_ab_ring_queues.txt).
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq);
   bool direct_done = false;
 #pragma unroll 1
   for (;;) {
-    uint32_t c0 = 0;
-    if (!work) {                                 // direct launch: value blockIdx.x, once
-      if (direct_done) break;
-      c0 = blockIdx.x;
-      direct_done = true;
+    uint32_t c0 = 0, cnt = 0;
+    if constexpr (kWQ) {
+      if (wq.cur >= wq.end) wq.claim();          // a direct launch: value blockIdx.x, once
+      if (wq.cur >= wq.end) break;
+      c0 = wq.cur;
+      cnt = wq.end - wq.cur;
+      wq.cur = wq.end;
     } else {
-      if (lane == 0) c0 = atomicAdd(work, batch);
-      c0 = uni(c0);
+      if (!work) {                               // direct launch: value blockIdx.x, once
+        if (direct_done) break;
+        c0 = blockIdx.x;
+        direct_done = true;
+      } else {
+        if (lane == 0) c0 = atomicAdd(work, batch);
+        c0 = uni(c0);
+      }
+      if (c0 >= n) break;
+      cnt = min(batch, n - c0);
     }
-    if (c0 >= n) break;
     const uint32_t vi = c0 + lane;
     bool mine = false;
-    if (lane < batch && vi < n) {
+    if (lane < cnt) {
       const uint32_t avail = in_len[vi];
       uint32_t osz = out_cap[vi], csz = avail;
       if (kFrame) {
@@ -914,11 +931,11 @@ __global__ __launch_bounds__(64) void lz4_decompress_big_kernel(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t prio) {
+    uint32_t prio, uint32_t nq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   if (prio) __builtin_amdgcn_s_setprio(2);     // a mixed batch's critical path (see launch_compress)
-  ring_decode_loop<kFrame, kORing, 8192u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
-                                   out_len, ret, work, batch);
+  ring_decode_loop<kFrame, kORing, 8192u, false>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                   out_len, ret, work, batch, nq);
 }
 
 // A batch with values on both sides of the LDS decoder's limit (a mixed
@@ -937,8 +954,8 @@ __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work_big, uint32_t batch_big,
     uint32_t* __restrict__ work_small, uint32_t batch_small, uint32_t nq) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  ring_decode_loop<kFrame, 4096u, kIR>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
-                                  out_len, ret, work_big, batch_big);
+  ring_decode_loop<kFrame, 4096u, kIR, kIR == 4096u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
+                                  out_len, ret, work_big, batch_big, nq);
   __syncthreads();
   small_decode_loop<kFrame, 5u>(smem, src, src_off, in_len, n, in_small, out_small, dst, dst_off, out_cap, target,
                             out_len, ret, work_small, batch_small, 1u, nq);
@@ -1082,7 +1099,7 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                                   std::to_string(R) + "u>";
   launch_note(name.c_str());
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, in_small, out_small, dst,
-                     dst_off, out_cap, target, out_len, ret, work, batch, prio);
+                     dst_off, out_cap, target, out_len, ret, work, batch, prio, work_queues(out_small));
   e = hipGetLastError();
   const hipError_t r = work_counter_release(st, work);
   return e != hipSuccess ? e : r;
