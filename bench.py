@@ -39,8 +39,8 @@ GIB = float(1 << 30)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--values", type=int, default=1 << 20, help="values per GPU")
     p.add_argument("--size", type=int, default=4096, help="bytes per value")
     p.add_argument("--workload", choices=("uniform", "mixed", "put", "get"), default="uniform",
