@@ -219,6 +219,19 @@ struct IntakeArena {
   uint64_t used = 0, cap = 0;
 };
 thread_local IntakeArena t_arena;
+// A client thread's per-pipeline state (Pipeline::thread_pipe): the shape of
+// its current value (Pipeline::regular) and its lane (Pipeline::lane_of).
+struct ThreadPipe {
+  struct Track {
+    bool open = false;       // the thread's last part left its value unfinished
+    uint64_t end = 0, size_value = 0;
+  } track;
+  struct LaneOf {
+    size_t lane;
+    uint64_t bytes;
+  } lane{0, 0};
+  bool lane_set = false;
+};
 std::atomic<uint64_t> g_pipeline_ids{1};
 // KDB_LZ4_FLUSH_STATS: when WriteBuffer::WritePart accounted this thread's last
 // deferred chunk (its lock and buffer-full wait come after that point)
@@ -323,12 +336,14 @@ constexpr uint64_t kLaneSpan = 2ull << 20;
 class Pipeline {
  public:
   explicit Pipeline(int device) : device_(device) {
-    // the lanes: this thread's device first, then the other visible ones
-    // (KDB_LZ4_FLUSH_DEVICES=<n> caps how many)
+    // the lanes: this thread's device (the one the caller bound with
+    // kdb_lz4_set_device) only, by default -- in a deployment of one process
+    // per GPU no process touches another's device; KDB_LZ4_FLUSH_DEVICES=<n>
+    // opts in to n lanes, this device first, then the next visible ones
     int count = 1;
     if (kdb_lz4_device_count(&count) != KDB_LZ4_OK || count < 1) count = 1;
     const char* cap = getenv("KDB_LZ4_FLUSH_DEVICES");
-    const long want = cap && *cap ? strtol(cap, nullptr, 10) : count;
+    const long want = cap && *cap ? strtol(cap, nullptr, 10) : 1;
     const int n = (int)std::max(1L, std::min<long>(count, want));
     for (int k = 0; k < n; k++) {
       lanes_.emplace_back(new Lane());
@@ -495,13 +510,7 @@ class Pipeline {
   // overlap, parts of two values interleaved on one thread, an empty chunk in
   // a value, a part after the value's end) is settled synchronously.
   bool regular(uint64_t offset_chunk, uint64_t cn, uint64_t size_value) {
-    struct Track {
-      uint64_t owner;                // Pipeline::id_
-      bool open;                     // the thread's last part left its value unfinished
-      uint64_t end, size_value;
-    };
-    thread_local Track t = {0, false, 0, 0};
-    if (t.owner != id_) t = Track{id_, false, 0, 0};
+    ThreadPipe::Track& t = thread_pipe().track;
     const bool bytes = cn > 0 && cn <= 0x7E000000ull;
     bool ok;
     if (offset_chunk == 0 && bytes) {
@@ -523,19 +532,33 @@ class Pipeline {
   // its lane until it has sent it kLaneSpan bytes, and moves on only at a
   // value's first part with bytes.
   size_t lane_of(uint64_t offset_chunk, uint64_t cn) {
-    struct LaneOf {
-      uint64_t owner;
-      size_t lane;
-      uint64_t bytes;
-    };
-    thread_local LaneOf t = {0, 0, 0};
-    if (t.owner != id_) t = LaneOf{id_, next_lane_.fetch_add(1, std::memory_order_relaxed) % lanes_.size(), 0};
+    ThreadPipe& tp = thread_pipe();
+    ThreadPipe::LaneOf& t = tp.lane;
+    if (!tp.lane_set) {
+      t = ThreadPipe::LaneOf{next_lane_.fetch_add(1, std::memory_order_relaxed) % lanes_.size(), 0};
+      tp.lane_set = true;
+    }
     if (lanes_.size() > 1 && offset_chunk == 0 && cn > 0 && t.bytes >= kLaneSpan) {
       t.lane = next_lane_.fetch_add(1, std::memory_order_relaxed) % lanes_.size();
       t.bytes = 0;
     }
     t.bytes += cn;
     return t.lane;
+  }
+
+  // This client thread's record for THIS pipeline (one per database: the
+  // reference keeps PutPartValidSize's state per Database and per thread, and
+  // a thread may interleave the parts of values in two databases).  Keyed by
+  // the pipeline id in a thread_local map, with the last pipeline cached, so
+  // switching databases never resets the other's lane or value tracking.
+  ThreadPipe& thread_pipe() {
+    thread_local uint64_t last_id = 0;
+    thread_local ThreadPipe* last = nullptr;
+    if (last_id == id_ && last) return *last;
+    thread_local std::unordered_map<uint64_t, ThreadPipe> all;
+    last = &all[id_];      // node-based: the reference stays valid across inserts
+    last_id = id_;
+    return *last;
   }
 
   // An irregular part waits for its own result (its lane is asked to take

@@ -272,9 +272,10 @@ struct StagingPool {
 };
 StagingPool g_read_pool;
 
-// The device a read-ahead batch decodes on: the batches of every iterator
-// take the visible devices in turn, starting from the asking thread's
-// (KDB_LZ4_READ_DEVICES=<n> caps how many); the batches are independent.
+// The device a read-ahead batch decodes on: the asking thread's by default
+// (one process per GPU touches no other device); KDB_LZ4_READ_DEVICES=<n>
+// opts in to n devices, which the batches of every iterator then take in
+// turn, starting from the asking thread's; the batches are independent.
 int read_device(int base) {
   static const int count = [] {
     int c = 1;
@@ -282,7 +283,7 @@ int read_device(int base) {
   }();
   static const int n = [] {
     const char* e = getenv("KDB_LZ4_READ_DEVICES");
-    const long want = e && *e ? atol(e) : count;
+    const long want = e && *e ? atol(e) : 1;
     return (int)std::max(1L, std::min<long>(count, want));
   }();
   static std::atomic<unsigned> next{0};

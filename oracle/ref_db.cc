@@ -191,8 +191,94 @@ static int readrandom(int argc, char** argv) {
   return f == (uint64_t)reads ? 0 : 1;
 }
 
+// ref_db --two <dirA> <dirB> <streamA.bin> <streamB.bin> [maximum_part_size [hstable_size [hash]]]:
+// ONE client thread writes two databases at once, part by part in turn (the
+// next part of stream A's current record, then the next of B's): each
+// database must end up with the files a run of its stream alone writes.  (The
+// reference keeps PutPartValidSize's state per Database and per thread,
+// database.cc:143-266, so interleaving the parts of values in two databases
+// is legal; the flush hook's per-thread lane and value tracking must be kept
+// per database too.)  Regular streams only (no explicit offsets).
+struct PartCursor {
+  FILE* f = nullptr;
+  std::string key;
+  uint64_t vsize = 0, off = 0;
+  uint32_t left = 0;
+  bool next(std::string* k, std::vector<char>* part, uint64_t* off_out, uint64_t* vs) {
+    while (left == 0) {
+      uint32_t klen;
+      if (fread(&klen, 4, 1, f) != 1) return false;
+      key.assign(klen, '\0');
+      if (!rd(f, &key[0], klen) || !rd(f, &vsize, 8) || !rd(f, &left, 4)) return false;
+      left &= 0x7FFFFFFFu;
+      off = 0;
+    }
+    uint32_t clen;
+    if (!rd(f, &clen, 4)) return false;
+    part->resize(clen);
+    if (!rd(f, part->data(), clen)) return false;
+    *k = key;
+    *off_out = off;
+    *vs = vsize;
+    off += clen;
+    left--;
+    return true;
+  }
+};
+
+static int two(int argc, char** argv) {
+  kdb::Logger::set_current_level("emerg");
+  kdb::DatabaseOptions options;
+  options.compression = kdb::kLZ4Compression;
+  if (argc > 6) options.storage__maximum_part_size = strtoull(argv[6], nullptr, 0);
+  if (argc > 7) options.storage__hstable_size = strtoull(argv[7], nullptr, 0);
+  if (argc > 8) options.hash = strtoul(argv[8], nullptr, 0) ? kdb::kxxHash_64 : kdb::kMurmurHash3_64;
+  kdb::Database da(options, argv[2]), dbb(options, argv[3]);
+  kdb::Database* db[2] = {&da, &dbb};
+  PartCursor cur[2];
+  for (int i = 0; i < 2; i++) {
+    kdb::Status s = db[i]->Open();
+    if (!s.IsOK()) {
+      fprintf(stderr, "open %d: %s\n", i, s.ToString().c_str());
+      return 1;
+    }
+    cur[i].f = fopen(argv[4 + i], "rb");
+    if (!cur[i].f) return 1;
+  }
+  kdb::WriteOptions wo;
+  bool more[2] = {true, true};
+  uint64_t parts = 0;
+  while (more[0] || more[1]) {
+    for (int i = 0; i < 2; i++) {
+      if (!more[i]) continue;
+      std::string key;
+      std::vector<char> part;
+      uint64_t off, vs;
+      if (!cur[i].next(&key, &part, &off, &vs)) {
+        more[i] = false;
+        continue;
+      }
+      kdb::ByteArray k = kdb::NewDeepCopyByteArray(key.data(), key.size());
+      kdb::ByteArray v = kdb::NewDeepCopyByteArray(part.data(), part.size());
+      kdb::Status s = db[i]->PutPart(wo, k, v, off, vs);
+      if (!s.IsOK()) {
+        fprintf(stderr, "db %d part %llu: %s\n", i, (unsigned long long)parts, s.ToString().c_str());
+        return 1;
+      }
+      parts++;
+    }
+  }
+  for (int i = 0; i < 2; i++) {
+    fclose(cur[i].f);
+    db[i]->Close();
+  }
+  printf("%llu parts into two databases\n", (unsigned long long)parts);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 4 && !strcmp(argv[1], "--verify")) return verify(argc, argv);
+  if (argc >= 6 && !strcmp(argv[1], "--two")) return two(argc, argv);
   if (argc >= 6 && !strcmp(argv[1], "--readrandom")) return readrandom(argc, argv);
   if (argc < 3) {
     fprintf(stderr, "usage: ref_db <dbdir> <stream.bin> [maximum_part_size [hstable_size [hash [none]]]]\n");

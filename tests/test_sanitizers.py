@@ -99,7 +99,8 @@ def test_kingdb_hook_threads_tsan(tmp_path, devices):
     _make(["-C", ORACLE, "kingdb_san", "SAN=thread"])
     # small read-ahead batches, so the iteration runs its helper threads too
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=0 exitcode=0 history_size=4", KDB_LZ4_READ_BATCH="32",
-               KDB_LZ4_CPU_MODEL_DEVICES=str(devices), KDB_LZ4_CPU_MODEL_STATS="1", KDB_LZ4_FLUSH_STATS="1")
+               KDB_LZ4_CPU_MODEL_DEVICES=str(devices), KDB_LZ4_FLUSH_DEVICES=str(devices),
+               KDB_LZ4_READ_DEVICES=str(devices), KDB_LZ4_CPU_MODEL_STATS="1", KDB_LZ4_FLUSH_STATS="1")
     r = subprocess.run([os.path.join(ORACLE, "_ref", "kingdb_tsan", "hook_mt"), str(tmp_path / "db"), "4", "60"],
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
