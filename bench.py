@@ -56,7 +56,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU leg")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--host-inclusive", action="store_true",
-                   help="also time pinned host -> device -> host (H2D + kernels + D2H, overlapped)")
+                   help="(default for the uniform workload) also time pinned host -> device -> host "
+                        "(H2D + kernels + D2H, overlapped)")
+    p.add_argument("--no-host-inclusive", action="store_true", help="skip the host-inclusive leg")
     p.add_argument("--hi-chunk", type=int, default=1 << 16, help="values per pipeline chunk")
     p.add_argument("--hi-streams", type=int, default=4)
     p.add_argument("--put-chunk", type=int, default=1 << 17, help="put workload: puts per pipeline chunk")
@@ -587,6 +589,9 @@ def main() -> None:
     for _ in range(args.warmup):
         batch.compress(stream)
         batch.decompress(stream)
+    # every output of the passes poisoned after the warm-ups (outside the timed
+    # region): the check after the loop then proves the timed steps wrote them
+    batch.poison(stream)
     stream.sync()
 
     evs = [[K.Event() for _ in range(3)] for _ in range(args.steps)]
@@ -704,7 +709,10 @@ def main() -> None:
         "decompress_gibs": round(raw / (d_ms * 1e-3) / GIB, 2),
         "cpu_baseline": None,
     }
-    if args.host_inclusive and args.workload == "uniform":
+    line["verify"] = ("every decoded byte and status checked after the timed steps; frames, decoded bytes, "
+                      "lengths and status words were poisoned before them" if not args.no_verify else
+                      "statuses and lengths only (poisoned before the timed steps)")
+    if not args.no_host_inclusive and args.workload == "uniform" and world == 1:
         line["host_inclusive"] = host_inclusive(batch, n, size, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "uniform":
         ncpu = min(n, 131072)

@@ -6,6 +6,7 @@
 // (pinned host + device buffers + a private stream) that grows on demand.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -30,8 +31,9 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* target, uint32_t* out_len, int32_t* ret);
 hipError_t launch_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed,
                          hipStream_t st);
-hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
-hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
+hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks);
+hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks,
+                                   uint64_t life_ticks);
 }  // namespace kdb_lz4
 
 using namespace kdb_lz4;
@@ -181,9 +183,14 @@ struct Service {
   bool ok = false;
   int device = 0;
   bool launch() {            // (mu held) a new instance, behind any old one on the stream
-    __atomic_store_n(&box->alive, 1u, __ATOMIC_SEQ_CST);
-    const hipError_t e = kind == kSvcDecode ? launch_decode_service(stream, dbox, idle_ticks, life_ticks)
-                                            : launch_compress_service(stream, dbox, idle_ticks, life_ticks);
+    // its generation (never 0) marks `alive` as its own: an older instance
+    // that exits later leaves it alone (service.h)
+    uint32_t gen = box->gen + 1u;
+    if (gen == 0u) gen = 1u;
+    box->gen = gen;
+    __atomic_store_n(&box->alive, gen, __ATOMIC_SEQ_CST);
+    const hipError_t e = kind == kSvcDecode ? launch_decode_service(stream, dbox, gen, idle_ticks, life_ticks)
+                                            : launch_compress_service(stream, dbox, gen, idle_ticks, life_ticks);
     if (e != hipSuccess) {
       __atomic_store_n(&box->alive, 0u, __ATOMIC_SEQ_CST);
       return false;
@@ -307,6 +314,10 @@ Lease lease_of(int dev, int kind) {
     if (!s->free_slots.empty()) {
       got = Lease{s, s->free_slots.back()};
       s->free_slots.pop_back();
+      // how many posts the wave's polls read (service.h): the leased slots'
+      const uint32_t hi = (uint32_t)got.slot + 1u;
+      if (hi > __atomic_load_n(&s->box->active, __ATOMIC_RELAXED))
+        __atomic_store_n(&s->box->active, std::min(hi, kSvcPostSlots), __ATOMIC_RELEASE);
     }
   }
   lease.slot[key] = got;
@@ -327,12 +338,24 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   Service* s = ls.s;
   const int k = ls.slot;
   SvcSlot& sl = s->box->slot[k];
-  SvcArgs& a = s->box->args[k];
-  a.csize = in_len;
-  a.osize = cap;
-  a.target = (uint32_t)target;
-  if (in_len) memcpy(sl.in, source, in_len);
   const uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
+  if ((uint32_t)k < kSvcPostSlots) {
+    // the post: arguments and (up to kSvcInline bytes) the input, then tag1,
+    // then tag0 -- each line's tag after its bytes (service.h)
+    SvcPost& p = s->box->post[k];
+    p.csize = in_len;
+    p.osize = cap;
+    p.target = (uint32_t)target;
+    if (in_len) memcpy(in_len <= kSvcInline ? p.data : sl.in, source, in_len);
+    __atomic_store_n(&p.tag1, want, __ATOMIC_RELEASE);
+    __atomic_store_n(&p.tag0, want, __ATOMIC_RELEASE);
+  } else {
+    SvcArgs& a = s->box->args[k];
+    a.csize = in_len;
+    a.osize = cap;
+    a.target = (uint32_t)target;
+    if (in_len) memcpy(sl.in, source, in_len);
+  }
   __atomic_store_n(&s->box->req[k], want, __ATOMIC_RELEASE);     // the doorbell, after the arguments
   __atomic_thread_fence(__ATOMIC_SEQ_CST);                        // ... and before alive is read
   s->ensure_running();

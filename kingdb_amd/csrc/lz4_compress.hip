@@ -319,11 +319,23 @@ __device__ __forceinline__ uint32_t vgpr_u32(uint32_t x) {
   return x;
 }
 
+// Inclusive sum over the wave's 64 lanes (DPP: row shifts inside each row of
+// 16, then the row totals broadcast into the rows above).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
 // points), like the reference.
-template <bool kWide, bool kGuard, class Src, class Tab>
+template <bool kWide, bool kGuard, bool kBatchE = false, class Src, class Tab>
 __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& tab,
                                               uint8_t* __restrict__ out, int out_cap, int cap) {
   const uint32_t lane = lane_id();
@@ -408,6 +420,83 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // always valid, lane 1 never; for a match lanes 0 and 1 never
     const int key_put = lane == 1u ? INT32_MAX : (lane == 0u || lane == 2u) ? INT32_MIN : (int)lane;
     const int key_match = lane <= 1u ? INT32_MAX : lane == 2u ? INT32_MIN : (int)lane;
+    // Batched emission (round 5; LDS-staged values, no limitedOutput cap):
+    // the parse only records each sequence -- lit | ml << 16 and the offset
+    // in lane `nseq` of two VGPRs (v_writelane from the SGPRs the search and
+    // the count leave) -- and flush_batch() encodes up to 64 sequences at
+    // once: one lane per sequence computes its exact run lengths and encoded
+    // size, a wave prefix sum gives every sequence's output and input
+    // positions, each lane stores its token, run bytes and offset, and the
+    // literal runs are copied LDS -> HBM one sequence per wave-wide store.
+    // The encoding's ~40 vector instructions per sequence leave the parse's
+    // chain.  (lz4.cc:535-592: the same bytes.)
+#ifndef KDB_LZ4_BATCH_EMIT
+#define KDB_LZ4_BATCH_EMIT 1
+#endif
+    constexpr bool kBatch = KDB_LZ4_BATCH_EMIT && kBatchE && kFree && !kGuard && !kWide;
+    uint32_t rlm = 0, roff = 0;       // lane k: sequence k of the batch (lit | ml << 16, offset)
+    uint32_t nseq = 0, banchor = 0;   // sequences recorded; the batch's first anchor
+    auto flush_batch = [&]() {
+      const bool on = lane < nseq;
+      const uint32_t L = on ? (rlm & 0xffffu) : 0u, M = on ? (rlm >> 16) : 0u;
+      const uint32_t nl1 = run_bytes(L), nm1 = run_bytes(M);
+      // encoded bytes | input bytes << 16 (each total < 2^16: S <= 8 KiB here)
+      const uint32_t x = on ? (L + nl1 + nm1 + 3u) | ((L + kMinMatch + M) << 16) : 0u;
+      const uint32_t xi = wave_incl_sum(x);
+      const uint32_t ex = xi - x;
+      const uint32_t o = (uint32_t)op + (ex & 0xffffu);   // the token
+      const uint32_t a = banchor + (ex >> 16);             // the literals in the value
+      const uint32_t lp = o + 1u + nl1;                    // the literals in the block
+      const uint32_t po = lp + L;                          // the offset (LE16)
+      auto st8 = [&](uint32_t v, bool w, uint32_t pos) {
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, out_rsrc, w ? (int)pos : (int)0x80000000, 0, 0);
+      };
+      st8((min(L, kRunMask) << 4) | min(M, kMlMask), on, o);
+      st8(roff, on, po);
+      st8(roff >> 8, on, po + 1u);
+      // the length runs: 255s, then run_last (lz4.cc:539-545, 582-590)
+#pragma unroll 1
+      for (uint32_t j = 0; ballot(j < max(nl1, nm1)) != 0; ++j) {
+        st8(j + 1u == nl1 ? run_last(L, nl1) : 255u, j < nl1, o + 1u + j);
+        st8(j + 1u == nm1 ? run_last(M, nm1) : 255u, j < nm1, po + 2u + j);
+      }
+      // the literals: one wave-wide byte store per sequence (its first 64),
+      // in passes of G sequences with their LDS reads issued together (eight
+      // while eight are left, then two: a sequence past nseq has L = 0 and
+      // stores nothing); the block position goes in the store's scalar
+      // offset.  Positions < 2^16: packed.
+      const uint32_t la = lp | (a << 16);
+      auto lit_pass = [&](uint32_t s0, auto g_c) {
+        constexpr uint32_t G = decltype(g_c)::value;
+        uint32_t b[G], vo[G], so[G];
+#pragma unroll
+        for (uint32_t k = 0; k < G; ++k) {
+          const uint32_t Ls = readlane(L, s0 + k), pk = readlane(la, s0 + k);
+          b[k] = src.u8((pk >> 16) + lane);
+          vo[k] = lane < Ls ? lane : 0x80000000u;
+          so[k] = pk & 0xffffu;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < G; ++k)
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)b[k], out_rsrc, (int)vo[k], (int)so[k], 0);
+      };
+      uint32_t s0 = 0;
+#pragma unroll 1
+      for (; s0 + 8u <= nseq; s0 += 8u) lit_pass(s0, std::integral_constant<uint32_t, 8>{});
+#pragma unroll 1
+      for (; s0 < nseq; s0 += 2u) lit_pass(s0, std::integral_constant<uint32_t, 2>{});   // s0 + 1 <= 63
+      // literal runs longer than 64 bytes (rare): the rest, sequence by sequence
+      for (uint64_t lng = ballot(L > 64u); lng; lng &= lng - 1u) {
+        const uint32_t s = (uint32_t)__builtin_ctzll(lng);
+        const uint32_t Ls = readlane(L, s), pk = readlane(la, s);
+#pragma unroll 1
+        for (uint32_t j = 64u; j < Ls; j += 64u)
+          st8(src.u8((pk >> 16) + j + lane), j + lane < Ls, (pk & 0xffffu) + j + lane);
+      }
+      op += (int)(readlane(xi, 63) & 0xffffu);
+      banchor = anchor;
+      nseq = 0;
+    };
     // The rest of a sequence once its search found a match (mm: the matching
     // lanes, pk/refk/slot: the chunk's positions, entries and table slots).
     auto finish = [&](uint64_t mm, uint32_t pk, uint32_t refk, const typename Tab::Slot& slot) {
@@ -570,6 +659,13 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         emit_seq<kGuard>(out, out_cap, seq_op, token, lit, nl1, remL, src, S, anchor, true, moff, nm1, remM);
         anchor = ip_end;
         seq0 = src.rd32_issue(clamp4(ip_end - 2u + lane));
+      } else if constexpr (kBatch) {
+        // record the sequence; its bytes are written by flush_batch
+        anchor = ip_end;
+        seq0 = src.rd32_issue(ip_end - 2u + lane);
+        rlm = writelane(lit | (ml << 16), nseq, rlm);
+        roff = writelane(moff, nseq, roff);
+        ++nseq;
       } else {
         // The encoding's arithmetic on the vector unit, on uniform VGPR
         // copies of lit and ml (the CU's one scalar unit, shared by its
@@ -756,7 +852,15 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // (lead) chunk, positions ip-2+lane (seq0 above).  The test is made here,
     // at the branch, so no flag carries it across the sequence's byte store.
 #pragma unroll 1
-    while (anchor < lim_end) sequence(std::true_type{});
+    while (anchor < lim_end) {
+      sequence(std::true_type{});
+      if constexpr (kBatch) {
+        if (nseq == 64u) flush_batch();
+      }
+    }
+    if constexpr (kBatch) {
+      if (nseq) flush_batch();
+    }
     if (kGuard && guard_fail) return 0;
   }
 
@@ -772,6 +876,17 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
 }
 
 constexpr uint32_t kSmallMax = 4096u;     // tagged table + register prefetch
+// Values from here on take compress_block's batched emission; shorter ones
+// (a few sequences: 100-byte values have one or two) emit each sequence as
+// it goes -- the batch flush's fixed cost (a prefix sum, the run-byte loop, a
+// pass of eight literal stores) is more than their per-sequence emission.
+// Two instances of the parse in one kernel, picked per value (a runtime
+// choice per sequence inside one instance moved ~12 instructions per
+// sequence to the scalar unit: headline compress 8.48 -> 8.83 ms).
+#ifndef KDB_LZ4_BATCH_MIN
+#define KDB_LZ4_BATCH_MIN 512
+#endif
+constexpr uint32_t kBatchMin = KDB_LZ4_BATCH_MIN;
 constexpr uint32_t kMidLdsMax = 8192u;    // LDS-staged values up to here, in place above
 constexpr uint32_t kPrefetch = 4u;        // output chunks per lane: 4096 / 16 / 64
 
@@ -794,7 +909,11 @@ __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint
 // The values of [min_len, in_cap] bytes, staged in LDS at `smem` (kSmall:
 // the fixed 16 KiB layout -- Table12, then the value; else Table16, then the
 // value), taken from the WorkQueue on `work`.
-template <bool kFrame, bool kSmall>
+// kEmit: how compress_block emits its sequences -- kEmitDirect (each as it
+// goes), kEmitBatch (batched), or kEmitPerValue (two instances of the parse,
+// batched for values of kBatchMin bytes and more).
+constexpr uint32_t kEmitDirect = 0, kEmitBatch = 1, kEmitPerValue = 2;
+template <bool kFrame, bool kSmall, uint32_t kEmit>
 __device__ __forceinline__ void values_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
@@ -889,12 +1008,16 @@ __device__ __forceinline__ void values_loop(
     if (!kFrame) {
       const uint32_t cap = uni(dst_cap[v]);
       LdsSrc ls{s_in};
+      const bool batch = kEmit == kEmitBatch || (kEmit == kEmitPerValue && S >= kBatchMin);
       const int r = cap < bound ? compress_block<false, true>(ls, S, tab, o, (int)cap, (int)cap)
-                                : compress_block<false, false>(ls, S, tab, o, (int)bound, (int)cap);
+                    : batch     ? compress_block<false, false, kEmit != kEmitDirect>(ls, S, tab, o, (int)bound, (int)cap)
+                                : compress_block<false, false, kEmit == kEmitBatch>(ls, S, tab, o, (int)bound, (int)cap);
       if (lane == 0) ret[v] = r;
     } else {
       LdsSrc ls{s_in};
-      const int r = compress_block<false, false>(ls, S, tab, o + 8, (int)bound, (int)bound);
+      const bool batch = kEmit == kEmitBatch || (kEmit == kEmitPerValue && S >= kBatchMin);
+      const int r = batch ? compress_block<false, false, kEmit != kEmitDirect>(ls, S, tab, o + 8, (int)bound, (int)bound)
+                          : compress_block<false, false, kEmit == kEmitBatch>(ls, S, tab, o + 8, (int)bound, (int)bound);
       if (r <= 0) {                              // compressor.cc:31-34
         if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
       } else {
@@ -921,7 +1044,7 @@ __device__ __forceinline__ void values_loop(
   }
 }
 
-template <bool kFrame, bool kSmall>
+template <bool kFrame, bool kSmall, uint32_t kEmit>
 __global__ __launch_bounds__(64) void lz4_compress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
@@ -936,7 +1059,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u : 16u;
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
-  values_loop<kFrame, kSmall>(kSmall ? smem_s : smem_d, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
+  values_loop<kFrame, kSmall, kEmit>(kSmall ? smem_s : smem_d, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                               dst_cap, frame_len, ret, work, batch, nq, guide);
 }
 
@@ -948,14 +1071,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 // as lz4_compress_kernel<false, true> stages it, the block written straight to
 // the slot in host memory.  Every wave reaches an exit: idle_ticks without a
 // request, life_ticks in all, or the host's stop.
-__device__ __forceinline__ uint32_t csys_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint32_t csys_peek(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, uint64_t idle_ticks,
+__global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, uint32_t gen, uint64_t idle_ticks,
                                                                   uint64_t life_ticks) {
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kTable12Bytes + kSmallMax];   // the kernel's only LDS
   const uint32_t lane = lane_id();
@@ -964,74 +1080,28 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
   for (uint32_t i = lane; i < kTable12Bytes / 16u; i += 64u) reinterpret_cast<uint4*>(s_tab)[i] = z4;
   __syncthreads();
   Table12 tab;
-  uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
-  const uint64_t t0 = wall_clock64();
-  uint64_t t_last = t0;
-  uint32_t served = 0;
-  // serves every slot of `pend` (their doorbells read as r)
-  auto serve = [&](uint64_t pend, uint32_t r) {
-#pragma unroll 1
-    while (pend) {
-      const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
-      pend &= pend - 1u;
-      const uint32_t want = readlane(r, sidx);
+  // the value staged at LDS [0, S) by svc_loop
+  svc_loop(box, gen, idle_ticks, life_ticks, smem_s, kSmallMax, [&](uint32_t sidx, const SvcArgs& a) -> int {
+    const uint32_t S = a.csize, cap = a.osize;
+    int rc = (int)kUnsupported;
+    if (S <= kSmallMax && cap <= kSvcOutBytes) {
+      __syncthreads();
+      const uint32_t bound = compress_bound(S);
+      LdsSrc ls{smem_s};
       SvcSlot* sl = &box->slot[sidx];
-      const SvcArgs a = svc_fetch(box, sidx, smem_s, kSmallMax);   // the value at LDS [0, S)
-      const uint32_t S = a.csize, cap = a.osize;
-      int rc = (int)kUnsupported;
-      if (S <= kSmallMax && cap <= kSvcOutBytes) {
-        __syncthreads();
-        const uint32_t bound = compress_bound(S);
-        LdsSrc ls{smem_s};
-        rc = cap < bound ? compress_block<false, true>(ls, S, tab, sl->out, (int)cap, (int)cap)
-                         : compress_block<false, false>(ls, S, tab, sl->out, (int)bound, (int)cap);
+      rc = cap < bound ? compress_block<false, true>(ls, S, tab, sl->out, (int)cap, (int)cap)
+                       : compress_block<false, false>(ls, S, tab, sl->out, (int)bound, (int)cap);
 #pragma unroll
-        for (uint32_t k = 0; k < kTable12Bytes / 1024u; ++k) reinterpret_cast<uint4*>(s_tab)[lane + 64u * k] = z4;
-        __syncthreads();
-      }
-      if (lane == 0)   // after the block: the request and its return value, one store
-        __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      if (lane == sidx) seen = want;
-      served++;
+      for (uint32_t k = 0; k < kTable12Bytes / 1024u; ++k) reinterpret_cast<uint4*>(s_tab)[lane + 64u * k] = z4;
+      __syncthreads();
     }
-  };
-#pragma unroll 1
-  for (;;) {
-    const uint32_t r = csys_load(&box->req[lane]);   // the 64 doorbells: one 256-byte read
-    const uint64_t pend = ballot(r != seen);
-    if (pend == 0) {
-      const uint64_t now = wall_clock64();
-      const bool stop = csys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
-      if (stop || old || now - t_last > idle_ticks) {
-        // leave: clear alive, then look at the doorbells once more.  A caller
-        // that rang before it read alive sees alive set, so it is served here
-        // (idle: and the wave goes on; at its end of life or at stop: these
-        // last ones, then it leaves); one that rang later sees it clear and
-        // launches the next instance, which queues behind this one.
-        if (lane == 0) __hip_atomic_store(&box->alive, 0u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-        __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        const uint32_t r2 = csys_load(&box->req[lane]);
-        const uint64_t pend2 = ballot(r2 != seen);
-        if (pend2 == 0) break;
-        serve(pend2, r2);
-        if (stop || old) break;
-        if (lane == 0) __hip_atomic_store(&box->alive, 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-        t_last = wall_clock64();
-        continue;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    serve(pend, r);
-    t_last = wall_clock64();
-  }
-  if (lane == 0)
-    __hip_atomic_store(&box->served, csys_peek(&box->served) + served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return rc;
+  });
 }
 
-hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
-  hipLaunchKernelGGL(lz4_compress_service_kernel, dim3(1), dim3(64), 0, st, box, idle_ticks, life_ticks);
+hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks,
+                                   uint64_t life_ticks) {
+  hipLaunchKernelGGL(lz4_compress_service_kernel, dim3(1), dim3(64), 0, st, box, gen, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 
@@ -1161,7 +1231,11 @@ __global__ __launch_bounds__(64) void lz4_compress_mixed_kernel(
   big_values<kFrame, false>(smem32, src, src_off, src_len, n, big_min, big_max, dst, dst_off, dst_cap, frame_len,
                             ret, work_big, batch_big);
   __syncthreads();
-  values_loop<kFrame, true>(reinterpret_cast<uint8_t*>(smem32), src, src_off, src_len, n, 0u, kSmallMax, dst,
+#ifndef KDB_LZ4_MIXED_EMIT
+#define KDB_LZ4_MIXED_EMIT kEmitPerValue
+#endif
+  // the small pass: 100-byte and 4 KiB values together, each its own form
+  values_loop<kFrame, true, KDB_LZ4_MIXED_EMIT>(reinterpret_cast<uint8_t*>(smem32), src, src_off, src_len, n, 0u, kSmallMax, dst,
                             dst_off, dst_cap, frame_len, ret, work_small, batch_small, nq, 0u);
 }
 
@@ -1193,20 +1267,29 @@ __global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n
   }
 }
 
-template <bool F, bool Sm>
+template <bool F, bool Sm, uint32_t Em>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0,
                              uint32_t guide = 0) {
-  auto kern = lz4_compress_kernel<F, Sm>;
+  auto kern = lz4_compress_kernel<F, Sm, Em>;
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t* work = nullptr;
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = claim_batch(n, grid);
-  launch_note(F ? (Sm ? "lz4_compress_kernel<true, true>" : "lz4_compress_kernel<true, false>")
-                : (Sm ? "lz4_compress_kernel<false, true>" : "lz4_compress_kernel<false, false>"));
+  // the rocprof (demangled) name
+  static const char* const names[2][2][3] = {
+      {{"lz4_compress_kernel<false, false, 0u>", "lz4_compress_kernel<false, false, 1u>",
+        "lz4_compress_kernel<false, false, 2u>"},
+       {"lz4_compress_kernel<false, true, 0u>", "lz4_compress_kernel<false, true, 1u>",
+        "lz4_compress_kernel<false, true, 2u>"}},
+      {{"lz4_compress_kernel<true, false, 0u>", "lz4_compress_kernel<true, false, 1u>",
+        "lz4_compress_kernel<true, false, 2u>"},
+       {"lz4_compress_kernel<true, true, 0u>", "lz4_compress_kernel<true, true, 1u>",
+        "lz4_compress_kernel<true, true, 2u>"}}};
+  launch_note(names[F][Sm][Em]);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap), guide);
   e = hipGetLastError();
@@ -1329,10 +1412,17 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     if (on[0] && !combo) {
       const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
       const uint32_t guide = claim_guide(min(max_len, kSmallMax));
-      r = frame ? launch_one<true, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                         frame_len, ret, census, 0, guide)
-                : launch_one<false, true>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst, dst_off, dst_cap,
-                                          frame_len, ret, census, 0, guide);
+      // batched emission when the launch may hold values of kBatchMin bytes
+      // and more (a launch of short values only keeps the per-sequence form)
+      const bool bat = max_len >= kBatchMin;
+      r = frame ? (bat ? launch_one<true, true, kEmitBatch>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                                                            dst_off, dst_cap, frame_len, ret, census, 0, guide)
+                       : launch_one<true, true, kEmitDirect>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                                                             dst_off, dst_cap, frame_len, ret, census, 0, guide))
+                : (bat ? launch_one<false, true, kEmitBatch>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                                                             dst_off, dst_cap, frame_len, ret, census, 0, guide)
+                       : launch_one<false, true, kEmitDirect>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                                                              dst_off, dst_cap, frame_len, ret, census, 0, guide));
       if (r != hipSuccess) return r;
     }
     // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
@@ -1341,10 +1431,10 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     if (on[1]) {
       const uint32_t top = min(max_len, hi[1]);
       const size_t lds = compress_lds_bytes(top);
-      r = frame ? launch_one<true, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
-                                          dst_cap, frame_len, ret, census, 1, claim_guide(top))
-                : launch_one<false, false>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
-                                           dst_cap, frame_len, ret, census, 1, claim_guide(top));
+      r = frame ? launch_one<true, false, kEmitBatch>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
+                                                      dst_cap, frame_len, ret, census, 1, claim_guide(top))
+                : launch_one<false, false, kEmitBatch>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
+                                                       dst_cap, frame_len, ret, census, 1, claim_guide(top));
     }
     return r;
   };

@@ -155,7 +155,8 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         asm("v_bfe_u32 %0, %1, 4, 4" : "=v"(ln) : "s"(tq));
         asm("v_bfe_u32 %0, %1, 8, 8" : "=v"(b1) : "s"(tq));
         lx = (ln + 1) >> 4;
-        xl = (int)((uint32_t)b1 * (uint32_t)lx);   // lx is 0 or 1: one v_mul_u32_u24, not a negate + and
+        xl = (int)__umul24((uint32_t)b1, (uint32_t)lx);   // lx is 0 or 1: one v_mul_u32_u24 (full
+                                                                           // rate), not v_mul_lo_u32, not a negate + and
         lit = ln + xl;                                            // <= 60 iff !lx || b1 <= 45
         als = atip + 1 + lx;
       };
@@ -608,7 +609,7 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
       auto header = [&](uint32_t tq, int tip) {
         const int ln = (int)(tq & 0xffu) >> 4, b1 = (int)((tq >> 8) & 0xffu);
         lx = (ln + 1) >> 4;
-        xl = (int)((uint32_t)b1 * (uint32_t)lx);   // lx is 0 or 1 (as in decode_block)
+        xl = (int)__umul24((uint32_t)b1, (uint32_t)lx);   // lx is 0 or 1 (as in decode_block)
         lit = ln + xl;
         ls = tip + 1 + lx;
       };
@@ -969,87 +970,29 @@ __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
 // exit: after idle_ticks of no requests, after life_ticks in all, or at the
 // host's stop.  Host memory is read and written with system-scope atomics
 // (doorbells, arguments, results) or plain vector loads/stores ordered by them.
-__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint32_t sys_peek(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v, int order) {
-  if (order == __ATOMIC_RELEASE) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  else __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
+__global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uint32_t gen, uint64_t idle_ticks,
+                                                                uint64_t life_ticks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   constexpr uint32_t s_in_cap = (kSvcMaxIn + 32u + 15u) & ~15u;   // small_decode_loop's layout
   uint8_t* s_in = smem;
   uint8_t* s_out = smem + s_in_cap;
-  // lane i: the last request of slot i served
-  uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
-  const uint64_t t0 = wall_clock64();
-  uint64_t t_last = t0;
-  uint32_t served = 0;
-  // serves every slot of `pend` (their doorbells read as r)
-  auto serve = [&](uint64_t pend, uint32_t r) {
-#pragma unroll 1
-    while (pend) {
-      const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
-      pend &= pend - 1u;
-      const uint32_t want = readlane(r, sidx);
-      // the arguments and the block, staged at s_in (head 0)
-      const SvcArgs a = svc_fetch(box, sidx, s_in, kSvcMaxIn);
-      const int csize = (int)a.csize, osize = (int)a.osize, tgt = (int)a.target;
-      int rc = (int)kUnsupported;
-      if (csize >= 0 && osize >= 0 && (uint32_t)csize <= kSvcMaxIn && (uint32_t)osize <= kSvcMaxOut) {
-        if (lane < 16u) s_in[(uint32_t)csize + lane] = 0;   // OOB bytes read as 0
-        __syncthreads();
-        rc = decode_block(s_in, 0u, csize, s_out, osize, tgt);
-        if (rc > 0) flush_lds_to_global(box->slot[sidx].out, s_out, 0, (uint32_t)rc);
-        __syncthreads();
-      }
-      if (lane == 0)   // after the bytes: the request and its return value, one store
-        __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      if (lane == sidx) seen = want;
-      served++;
+  // the block staged at s_in (head 0) by svc_loop
+  svc_loop(box, gen, idle_ticks, life_ticks, s_in, kSvcMaxIn, [&](uint32_t sidx, const SvcArgs& a) -> int {
+    const int csize = (int)a.csize, osize = (int)a.osize, tgt = (int)a.target;
+    int rc = (int)kUnsupported;
+    if (csize >= 0 && osize >= 0 && (uint32_t)csize <= kSvcMaxIn && (uint32_t)osize <= kSvcMaxOut) {
+      if (lane < 16u) s_in[(uint32_t)csize + lane] = 0;   // OOB bytes read as 0
+      __syncthreads();
+      rc = decode_block(s_in, 0u, csize, s_out, osize, tgt);
+      if (rc > 0) flush_lds_to_global(box->slot[sidx].out, s_out, 0, (uint32_t)rc);
+      __syncthreads();
     }
-  };
-#pragma unroll 1
-  for (;;) {
-    const uint32_t r = sys_load(&box->req[lane]);   // the 64 doorbells: one 256-byte read
-    const uint64_t pend = ballot(r != seen);
-    if (pend == 0) {
-      const uint64_t now = wall_clock64();
-      const bool stop = sys_peek(&box->stop) != 0u, old = now - t0 > life_ticks;
-      if (stop || old || now - t_last > idle_ticks) {
-        // leave: clear alive, then look at the doorbells once more.  A caller
-        // that rang before it read alive sees alive set, so it is served here
-        // (idle: and the wave goes on; at its end of life or at stop: these
-        // last ones, then it leaves); one that rang later sees it clear and
-        // launches the next instance, which queues behind this one.
-        if (lane == 0) sys_store(&box->alive, 0u, __ATOMIC_SEQ_CST);
-        __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        const uint32_t r2 = sys_load(&box->req[lane]);
-        const uint64_t pend2 = ballot(r2 != seen);
-        if (pend2 == 0) break;
-        serve(pend2, r2);
-        if (stop || old) break;
-        if (lane == 0) sys_store(&box->alive, 1u, __ATOMIC_SEQ_CST);
-        t_last = wall_clock64();
-        continue;
-      }
-      __builtin_amdgcn_s_sleep(2);
-      continue;
-    }
-    serve(pend, r);
-    t_last = wall_clock64();
-  }
-  if (lane == 0) sys_store(&box->served, sys_peek(&box->served) + served, __ATOMIC_RELEASE);
+    return rc;
+  });
 }
 
-hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks);
+hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks);
 
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
   // staged block (16 B alignment head + block + 16 zero bytes) | output window
@@ -1163,9 +1106,9 @@ constexpr uint32_t kMixedOutSmall8 = 6144u, kMixedOutSmall4 = 4096u;
 static_assert(kMixedOutSmall4 + kMixedOutSmall4 / 255u + 24u + 32u + 15u + kMixedOutSmall4 + 64u <= 4096u + 4096u + kIMirror,
               "the small pass's staging fits the 4 KiB input ring's LDS");
 
-hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint64_t idle_ticks, uint64_t life_ticks) {
+hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks) {
   const size_t lds = decompress_lds_bytes(kSvcMaxIn, kSvcMaxOut);
-  hipLaunchKernelGGL(lz4_decode_service_kernel, dim3(1), dim3(64), lds, st, box, idle_ticks, life_ticks);
+  hipLaunchKernelGGL(lz4_decode_service_kernel, dim3(1), dim3(64), lds, st, box, gen, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 

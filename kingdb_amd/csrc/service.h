@@ -1,29 +1,50 @@
-// kingdb_amd/csrc/service.h -- the resident decode service of the per-call
-// path (kdb_lz4_decompress_safe_partial, i.e. CompressorLZ4::Uncompress and
-// UncompressByteArray one frame at a time: /root/reference/algorithm/lz4.cc:
-// 1050-1053, compressor.cc:75-137).
+// kingdb_amd/csrc/service.h -- the resident services of the per-call path:
+// per-call decodes (kdb_lz4_decompress_safe_partial, i.e.
+// CompressorLZ4::Uncompress and UncompressByteArray one frame at a time:
+// /root/reference/algorithm/lz4.cc:1050-1053, compressor.cc:75-137) and
+// per-call compressions (kdb_lz4_compress_limitedOutput, lz4.cc:664-682).
 //
 // A launch + a stream sync per call cost ~16 us, almost
-// all of it the launch path, not the decode.  The service is one wave that
-// stays resident on the device while calls keep coming: a calling thread
-// writes its block into a slot of a pinned, coherent, device-mapped mailbox
-// and rings the slot's doorbell; the wave, polling the 64 doorbells with one
-// 256-byte read, decodes the block with the same decode_block as the batch
-// kernels (lz4_decompress.hip; lz4_compress.hip has the compress twin) and
-// writes the bytes and then the slot's done word (request and return code in
-// one store) back into host memory; the thread spins on the done word.  No
-// launch and no runtime call per request.
+// all of it the launch path, not the codec.  A service is one wave that stays
+// resident on the device while calls keep coming: a calling thread writes its
+// request into a slot of a pinned, coherent, device-mapped mailbox and rings
+// the slot's doorbell; the wave, polling the 64 doorbells, runs the request
+// with the same device code as the batch kernels (lz4_decompress.hip's
+// decode_block, lz4_compress.hip's compress_block) and writes the bytes and
+// then the slot's done word (request and return code in one store) back into
+// host memory; the thread spins on the done word.  No launch and no runtime
+// call per request.
 //
-// Lifetime: the host launches the wave (on a stream of its own, so two
-// instances never run at once) when it finds it gone (`alive` == 0).  The wave
-// exits after KDB_LZ4_SERVICE_IDLE_US (2 ms) without a request, after 20 ms in
-// all, or when the host sets `stop`; before leaving it clears `alive`, looks at the doorbells once more
-// and stays if a request slipped in (the host rings, then reads `alive`; the
-// wave clears `alive`, then reads the doorbells: one of them sees the other).
+// Per request the wave reads host memory over PCIe, so what a request waits
+// for is PCIe round trips (round 5):
+//  * each poll (relaxed system-scope loads, which bypass the caches) also reads the first kSvcPostSlots slots' POSTS: a 128-byte
+//    record per slot holding the request's arguments and, for inputs up to
+//    kSvcInline bytes (a 100-byte value, or its ~60-byte block), the input
+//    itself.  The host writes the post, then its two tags (one per 64-byte
+//    line: tag1 at the end of line 1, then tag0 at the start of line 0), then
+//    the doorbell.  A 64-byte line is read as one unit, so a line whose tag
+//    is the request's number holds that request's bytes; with both tags equal
+//    to the doorbell the wave takes the request straight from the poll -- no
+//    second round trip for its arguments and input.  Otherwise (larger
+//    inputs, slots past kSvcPostSlots, a post read before it was complete)
+//    the wave fetches them after an acquire fence, as before.
+//
+// Lifetime: the host launches an instance (on a stream of its own, so two
+// instances never run at once) when it finds `alive` == 0, and stores the
+// instance's generation in `alive` first.  The wave exits after
+// KDB_LZ4_SERVICE_IDLE_US (2 ms) without a request, after 20 ms in all, or
+// when the host sets `stop`; before leaving it clears `alive` -- only if it
+// still holds its own generation, so an old instance never clears the flag
+// of the one queued behind it -- then looks at the doorbells once more and
+// stays if a request slipped in (the host rings, then reads `alive`; the wave
+// clears `alive`, then reads the doorbells: one of them sees the other).
 // A caller whose request is not served within a bound relaunches it.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
+
+#include "lz4_device.h"
 
 namespace kdb_lz4 {
 
@@ -32,48 +53,94 @@ constexpr uint32_t kSvcMaxOut = 8192;        // the per-call zero-copy class (de
 constexpr uint32_t kSvcMaxIn = kSvcMaxOut + kSvcMaxOut / 255u + 24u;
 constexpr uint32_t kSvcInBytes = (kSvcMaxIn + 64u + 15u) & ~15u;
 constexpr uint32_t kSvcOutBytes = kSvcMaxOut + 64u;
+constexpr uint32_t kSvcPostSlots = 16;       // slots whose posts every poll reads (2 KiB)
+constexpr uint32_t kSvcInline = 108;         // input bytes a post carries
 
-// A request's arguments, in a row of their own (read with the block, right
-// after the doorbell): LZ4_decompress_safe_partial's (csize, osize, target)
+// A request's arguments: LZ4_decompress_safe_partial's (csize, osize, target)
 // or LZ4_compress_limitedOutput's (input bytes, output capacity).
 struct SvcArgs {
   uint32_t csize, osize, target, pad;
 };
 
+// A slot's post (slots < kSvcPostSlots): line 0 = tag0, the arguments and
+// input bytes [0, 48); line 1 = input bytes [48, 108) and tag1.
+struct SvcPost {
+  uint32_t tag0;
+  uint32_t csize, osize, target;
+  uint8_t data[kSvcInline];
+  uint32_t tag1;
+};
+static_assert(sizeof(SvcPost) == 128, "two 64-byte lines");
+
 struct SvcSlot {
-  uint8_t in[kSvcInBytes];         // the block / value (16-byte aligned)
+  uint8_t in[kSvcInBytes];         // the block / value (16-byte aligned), when not in the post
   uint8_t out[kSvcOutBytes];       // the result bytes
 };
 
-// Per request, three PCIe round trips on the wave's side: the doorbells (one
-// 256-byte read per poll), then the slot's arguments and the first KiB of its
-// input together (the rest, if any, one more), then the result bytes and one
-// 64-bit release store of (request << 32 | return value) into its done word.
 struct SvcBox {
   uint32_t req[kSvcSlots];         // host: a slot's request number (written last)
   uint64_t done[kSvcSlots];        // device: (request served << 32) | return value (written last)
-  SvcArgs args[kSvcSlots];         // host: the arguments of the slot's request
-  uint32_t alive;                  // host sets 1 before a launch; the wave clears it as it exits
+  SvcArgs args[kSvcSlots];         // host: the arguments of slots >= kSvcPostSlots
+  uint32_t alive;                  // host: the generation it launched last (0: none); the wave clears its own
   uint32_t stop;                   // host: exit now (process teardown)
   uint32_t launches, served;       // counters (diagnostics)
-  uint32_t pad[60];
+  uint32_t active;                 // host: 1 + the highest slot leased (how many posts a poll reads)
+  uint32_t gen;                    // host: the last generation launched
+  uint32_t polls, inline_served;   // device: counters (diagnostics)
+  uint32_t pad[56];
+  SvcPost post[kSvcPostSlots];     // 128-byte aligned (offset 2048)
   SvcSlot slot[kSvcSlots];
 };
+static_assert(offsetof(SvcBox, post) % 128 == 0 && offsetof(SvcBox, slot) % 16 == 0, "mailbox layout");
 
-// The wave's side of a request: the slot's arguments and its input (up to
-// max_in bytes) staged into LDS at `lds` (16-byte aligned; input byte i at
-// lds[i]).  The arguments and the first KiB go out together, one round trip;
-// the rest, if any, all in flight at once, one more.  Called right after the
-// doorbell's system-scope acquire load, which orders these reads after the
-// host's writes.
+__device__ __forceinline__ uint32_t svc_relaxed(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void svc_store(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+typedef uint32_t svc_u32x4 __attribute__((ext_vector_type(4)));
+
+// One poll: the 64 doorbells (lane l: slot l's), the host's `active`, and the
+// posts of the first 8 / 16 slots (lane l: bytes [16 l, 16 l + 16) of the
+// posts of slots 0-7, resp. 8-15).  Every load is relaxed at system scope
+// (sc0 sc1: past the caches).
+struct SvcPoll {
+  uint32_t r, act;
+  svc_u32x4 p0, p1;
+};
+__device__ __forceinline__ SvcPoll svc_poll(SvcBox* box, uint32_t act) {
+  const uint32_t lane = lane_id();
+  SvcPoll q;
+  q.r = svc_relaxed(&box->req[lane]);
+  q.act = svc_relaxed(&box->active);
+  // the same four loads every poll (so the wait for the older poll is a
+  // static count); posts past the leased slots lie past the buffer's range
+  // and read as 0 without touching memory.  Cache policy 17 = sc0 | sc1
+  // (system scope) on gfx950.
+  const __amdgpu_buffer_rsrc_t posts = __builtin_amdgcn_make_buffer_rsrc(
+      box->post, 0, (int)(128u * (act < kSvcPostSlots ? act : kSvcPostSlots)), 0x00020000);
+  q.p0 = __builtin_amdgcn_raw_buffer_load_b128(posts, (int)(16u * lane), 0, 17);
+  q.p1 = __builtin_amdgcn_raw_buffer_load_b128(posts, (int)(16u * lane + 1024u), 0, 17);
+  return q;
+}
+
+// The wave's side of a request whose post was not usable: its arguments and
+// input (up to max_in bytes) staged into LDS at `lds` (16-byte aligned; input
+// byte i at lds[i]).  The post (or the arguments row) and the first KiB of
+// the slot's input go out together, one round trip; the rest, if any, all in
+// flight at once, one more.  Called after an acquire fence that follows the
+// doorbell's load, which orders these reads after the host's writes.
 __device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t* lds, uint32_t max_in) {
-  const uint32_t lane = __lane_id();
-  SvcArgs* ap = &box->args[sidx];
-  const uint32_t cs = __hip_atomic_load(&ap->csize, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const uint32_t os = __hip_atomic_load(&ap->osize, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const uint32_t tg = __hip_atomic_load(&ap->target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint32_t lane = lane_id();
+  const bool posted = sidx < kSvcPostSlots;
+  const uint32_t* ap = posted ? &box->post[sidx].csize : &box->args[sidx].csize;
+  const uint32_t cs = svc_relaxed(ap), os = svc_relaxed(ap + 1), tg = svc_relaxed(ap + 2);
   const uint4* in4 = reinterpret_cast<const uint4*>(box->slot[sidx].in);
+  const uint4* pin4 = reinterpret_cast<const uint4*>(posted ? box->post[sidx].data : box->slot[sidx].in);
   const uint4 c0 = in4[lane];
+  const uint4 pc = lane < 7u ? pin4[lane] : make_uint4(0, 0, 0, 0);   // a post's input: 112 bytes from data
   SvcArgs a;
   a.csize = (uint32_t)__builtin_amdgcn_readfirstlane((int)cs);
   a.osize = (uint32_t)__builtin_amdgcn_readfirstlane((int)os);
@@ -82,6 +149,10 @@ __device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t
   const uint32_t n = a.csize < max_in ? a.csize : max_in;
   const uint32_t chunks = (n + 15u) >> 4;
   uint4* l4 = reinterpret_cast<uint4*>(lds);
+  if (posted && a.csize <= kSvcInline) {         // the input is in the post
+    if (lane < chunks) l4[lane] = pc;
+    return a;
+  }
   if (lane < chunks) l4[lane] = c0;
   constexpr uint32_t kMore = (kSvcInBytes / 16u + 63u) / 64u - 1u;
   if (chunks > 64u) {
@@ -94,6 +165,112 @@ __device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t
       if (lane + 64u * (k + 1u) < chunks) l4[lane + 64u * (k + 1u)] = r[k];
   }
   return a;
+}
+
+// The request of slot sidx (doorbell `want`) taken from poll q when its post
+// is complete: the arguments, and the input staged at lds[0, csize); false
+// when the post is not usable (then svc_fetch).
+__device__ __forceinline__ bool svc_from_post(const SvcPoll& q, uint32_t sidx, uint32_t want, uint8_t* lds,
+                                              SvcArgs* a) {
+  if (sidx >= kSvcPostSlots) return false;
+  const uint32_t lane = lane_id();
+  const uint32_t b = 8u * (sidx & 7u);           // the post's first lane
+  const bool hi = sidx >= 8u;
+  const uint32_t x = hi ? q.p1.x : q.p0.x, y = hi ? q.p1.y : q.p0.y, z = hi ? q.p1.z : q.p0.z,
+                 w = hi ? q.p1.w : q.p0.w;
+  const uint32_t tag0 = readlane(x, b), tag1 = readlane(w, b + 7u);
+  if (tag0 != want || tag1 != want) return false;
+  a->csize = readlane(y, b);
+  a->osize = readlane(z, b);
+  a->target = readlane(w, b);
+  a->pad = 0;
+  if (a->csize > kSvcInline) return false;        // the input is in the slot: fetch it
+  // lanes b+1 .. b+7 hold post bytes [16, 128): input bytes [0, 112)
+  if (lane > b && lane < b + 8u) reinterpret_cast<uint4*>(lds)[lane - b - 1u] = make_uint4(x, y, z, w);
+  return true;
+}
+
+// The service loop shared by both kinds: polls, takes each
+// pending slot's request (from its post, or fetched), runs serve(sidx, args)
+// -- the input at lds[0, csize), returning the return word after writing the
+// result bytes to box->slot[sidx].out -- then publishes (request << 32 | rc)
+// in the slot's done word.  Every wave reaches an exit: idle_ticks without a
+// request, life_ticks in all, or the host's stop.
+template <class Serve>
+__device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                                         uint8_t* lds, uint32_t max_in, Serve serve) {
+  const uint32_t lane = lane_id();
+  // lane i: the last request of slot i served
+  uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+  const uint64_t t0 = wall_clock64();
+  uint64_t t_last = t0;
+  uint32_t served = 0, polls = 0, inl = 0;
+  uint32_t act = kSvcPostSlots;
+  auto serve_pending = [&](uint64_t pend, const SvcPoll& q) {
+#pragma unroll 1
+    while (pend) {
+      const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1u;
+      const uint32_t want = readlane(q.r, sidx);
+      SvcArgs a;
+      if (svc_from_post(q, sidx, want, lds, &a)) {
+        inl++;
+      } else {
+        // the doorbell's writes before the fetch's plain loads (a relaxed
+        // load of the doorbell + this fence synchronise with its release)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        a = svc_fetch(box, sidx, lds, max_in);
+      }
+      const int rc = serve(sidx, a);
+      if (lane == 0)   // after the bytes: the request and its return value, one store
+        __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (lane == sidx) seen = want;
+      served++;
+    }
+  };
+  // One poll in flight at a time: a second one, issued while the first is
+  // looked at, would be waited for by the release of every request served
+  // (loads and stores share one in-order counter), costing more than it saves.
+#pragma unroll 1
+  for (;;) {
+    const SvcPoll q = svc_poll(box, act);
+    polls++;
+    act = uni(q.act);
+    const uint64_t pend = ballot(q.r != seen);
+    if (pend) {
+      serve_pending(pend, q);
+      t_last = wall_clock64();
+      continue;
+    }
+    const uint64_t now = wall_clock64();
+    const bool stop = svc_relaxed(&box->stop) != 0u, old = now - t0 > life_ticks;
+    if (!(stop || old || now - t_last > idle_ticks)) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    // leave: clear alive (when it is still this instance's), then look at
+    // the doorbells once more.  A caller that rang before it read alive sees
+    // alive set, so it is served here (idle: and the wave goes on; at its end
+    // of life or at stop: these last ones, then it leaves); one that rang
+    // later sees it clear and launches the next instance, which queues behind
+    // this one.
+    if (lane == 0 && svc_relaxed(&box->alive) == gen) svc_store(&box->alive, 0u);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    const SvcPoll q2 = svc_poll(box, act);
+    const uint64_t pend2 = ballot(q2.r != seen);
+    if (pend2 == 0) break;
+    serve_pending(pend2, q2);
+    if (stop || old) break;
+    if (lane == 0 && svc_relaxed(&box->alive) == 0u) svc_store(&box->alive, gen);
+    t_last = wall_clock64();
+  }
+  if (lane == 0) {
+    __hip_atomic_store(&box->served, svc_relaxed(&box->served) + served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->polls, svc_relaxed(&box->polls) + polls, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->inline_served, svc_relaxed(&box->inline_served) + inl, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 }  // namespace kdb_lz4

@@ -463,6 +463,17 @@ class DeviceBatch:
     def out_lens(self) -> np.ndarray:
         return self.meta.download(4 * self.n, 40 * self.n).view(np.uint32)
 
+    def poison(self, stream: Stream | None = None) -> None:
+        """Overwrite every output of compress() and decompress() -- frame slots,
+        decoded bytes, frame lengths, decoded lengths and both status words --
+        with bytes no correct pass leaves there (0xA5 / all ones), so that a
+        later roundtrip_ok() proves the passes after this call wrote them."""
+        st = stream.ptr if stream else None
+        n = self.n
+        for ptr, nbytes, val in ((self.frames.ptr, self.frames.nbytes, 0xA5), (self.out.ptr, self.out.nbytes, 0xA5),
+                                 (self._p(3), 8 * n, 0xFF), (self._p(7), 8 * n, 0xFF)):
+            _lib.check(lib().kdb_lz4_memset(ptr, val, nbytes, st), "memset")
+
     def roundtrip_ok(self) -> bool:
         """Every status 0, every decoded length right, every decoded byte equal."""
         cst, dst = self.status()

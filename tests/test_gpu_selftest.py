@@ -61,11 +61,13 @@ def test_last_kernels_names(gpu):
     return at once): the names are rocprof's."""
     import kingdb_amd as K
     K.compress_frames([b"x" * 4096] * 4)
-    assert K.last_kernels() == ["lz4_compress_kernel<true, true>"]
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u>"]   # batched emission
+    K.compress_frames([b"x" * 100] * 4)
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 0u>"]   # short values: per sequence
     K.compress_frames([b"x" * 6000] * 4)
-    assert K.last_kernels() == ["lz4_compress_kernel<true, true>", "lz4_compress_kernel<true, false>"]
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u>", "lz4_compress_kernel<true, false, 1u>"]
     K.compress_frames([b"x" * 4096, b"y" * 20000])
-    assert K.last_kernels() == ["lz4_compress_mixed_kernel<true>", "lz4_compress_kernel<true, false>"]
+    assert K.last_kernels() == ["lz4_compress_mixed_kernel<true>", "lz4_compress_kernel<true, false, 1u>"]
     K.compress_frames([b"x" * 100000])
     assert "lz4_compress_big_kernel<true, true>" in K.last_kernels()
     K.decompress_frames(K.compress_frames([b"x" * 4096] * 4), [4096] * 4)

@@ -46,7 +46,7 @@ prof() {  # prof <name> <bench args...>
 pmc() {  # pmc <name> <n_values> <size> <bench args...>
   local n=$1 nv=$2 sz=$3; shift 3
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/${O}_pmc_${n}_$c" -o pmc -- python3 "$R/bench.py" --no-cpu-baseline --no-verify --steps 1 --warmup 0 "$@" > "${O}_pmc_${n}_$c.log" 2>&1 || fail "pmc $n $c" $? "${O}_pmc_${n}_$c.log"
+    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/${O}_pmc_${n}_$c" -o pmc -- python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --no-verify --steps 1 --warmup 0 "$@" > "${O}_pmc_${n}_$c.log" 2>&1 || fail "pmc $n $c" $? "${O}_pmc_${n}_$c.log"
   done
   python tools/pmc_traffic.py "${O}_pmc_${n}_FETCH_SIZE" "${O}_pmc_${n}_WRITE_SIZE" "$nv" "$sz" "${O}_pmc_traffic_$n.json" || exit 1
   cat "${O}_pmc_traffic_$n.json"
@@ -64,12 +64,12 @@ for s in "$@"; do
       timeout -k 10 600 python bench.py --host-inclusive > "${O}_bench.json" 2> "${O}_bench.err" || fail bench $? "${O}_bench.err"
       cat "${O}_bench.json" ;;
     quick)
-      timeout -k 10 300 python bench.py --no-cpu-baseline > "${O}_quick.json" 2> "${O}_quick.err" || fail quick $? "${O}_quick.err"
+      timeout -k 10 300 python bench.py --no-cpu-baseline --no-host-inclusive > "${O}_quick.json" 2> "${O}_quick.err" || fail quick $? "${O}_quick.err"
       line "${O}_quick.json" ;;
     mixed|put|get)
       timeout -k 10 500 python bench.py --workload $s > "${O}_$s.json" 2> "${O}_$s.err" || fail $s $? "${O}_$s.err"
       cat "${O}_$s.json" ;;
-    prof) prof bench --no-cpu-baseline --steps 5 --warmup 1 ;;
+    prof) prof bench --no-cpu-baseline --no-host-inclusive --steps 5 --warmup 1 ;;
     profmixed) prof mixed --workload mixed --no-cpu-baseline --steps 3 --warmup 1 ;;
     profput) prof put --workload put --no-cpu-baseline --steps 3 --warmup 1 ;;
     profget) prof get --workload get --no-cpu-baseline --steps 3 --warmup 1 ;;
@@ -79,7 +79,7 @@ for s in "$@"; do
       a=${s#pmcu:}; sz=${a%%:*}; nv=${a#*:}
       pmc u${sz} $nv $sz --size $sz --values $nv ;;
     sq)
-      timeout -k 10 900 bash tools/pmc.sh "${O}_sq" python3 "$R/bench.py" --no-cpu-baseline --no-verify --steps 1 --warmup 0 || exit 1
+      timeout -k 10 900 bash tools/pmc.sh "${O}_sq" python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --no-verify --steps 1 --warmup 0 || exit 1
       python tools/pmc_summary.py "${O}_sq" > "${O}_sq.txt" && cat "${O}_sq.txt" ;;
     dropin|dropinfull)
       [ $s = dropinfull ] && export KDB_DROPIN_FULL=1
@@ -117,7 +117,7 @@ for s in "$@"; do
       cat "${O}_var_$v.txt" ;;
     ab:*)
       kv=${s#ab:}
-      env "$kv" timeout -k 10 300 python bench.py --no-cpu-baseline > "${O}_ab_${kv}.json" 2> "${O}_ab.err" || fail "ab $kv" $? "${O}_ab.err"
+      env "$kv" timeout -k 10 300 python bench.py --no-cpu-baseline --no-host-inclusive > "${O}_ab_${kv}.json" 2> "${O}_ab.err" || fail "ab $kv" $? "${O}_ab.err"
       line "${O}_ab_${kv}.json" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
