@@ -32,6 +32,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "LZ4 compress+decompress GiB/s (device-resident), batched 4 KiB values, 1/8 GPU"
+# --workload big: the same round trip on KingDB's default part size (a side line, not the headline)
+METRIC_BIG = "LZ4 compress+decompress GiB/s (device-resident), KingDB 1 MiB parts (byU32 blocks), 1/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = float(1 << 30)
 
@@ -41,14 +43,17 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--values", type=int, default=1 << 20, help="values per GPU")
-    p.add_argument("--size", type=int, default=4096, help="bytes per value")
-    p.add_argument("--workload", choices=("uniform", "mixed", "put", "get"), default="uniform",
+    p.add_argument("--values", type=int, default=None, help="values per GPU (default 1 Mi; big: 2560)")
+    p.add_argument("--size", type=int, default=None, help="bytes per value (default 4096; big: 1 MiB)")
+    p.add_argument("--workload", choices=("uniform", "mixed", "put", "get", "big"), default="uniform",
                    help="uniform: --values x --size (configs[2], the headline); mixed: configs[3], "
                         "--values per GPU of 90%% 100 B / 9%% 4 KiB / 1%% 64 KiB parts, byte-balanced shards; "
                         "put: configs[4], --values puts per GPU of 16 B keys / 100 B values from pinned host "
                         "memory to HSTable file bytes in host memory; get: the read path (configs[1] shape), "
-                        "UncompressByteArray over --values stored --size B values resident in HBM")
+                        "UncompressByteArray over --values stored --size B values resident in HBM; big: KingDB's "
+                        "default part size (util/options.h:171-172: 1 MB parts, byU32 blocks, lz4.cc:673-676), "
+                        "--values x --size B as the uniform workload (default 2560 x 1 MiB: one part per wave "
+                        "slot of the in-place kernels, 10 per CU)")
     p.add_argument("--put-host-copy", action="store_true",
                    help="put workload: land entry bytes in a pinned staging buffer and memcpy them into the "
                         "files (the default DMAs them from HBM straight into pinned file buffers)")
@@ -65,7 +70,12 @@ def parse():
     p.add_argument("--pmc", default=None,
                    help="HBM traffic summary written by tools/pmc_traffic.py (default: "
                         "profiles/pmc_traffic.json, profiles/pmc_traffic_mixed.json for --workload mixed)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.values is None:
+        a.values = 2560 if a.workload == "big" else 1 << 20
+    if a.size is None:
+        a.size = 1 << 20 if a.workload == "big" else 4096
+    return a
 
 
 def cpu_model() -> str:
@@ -650,11 +660,11 @@ def main() -> None:
         want = (args.values, "mixed") if args.workload == "mixed" else (n, size)
         got = pm["kernels"][dom_key]
         got_names = set(k.replace("kdb_lz4::", "") for k in (got.get("kernel") or "").split(" + "))
-        if (pm.get("values"), pm.get("size")) != want or not (world == 1 or args.workload == "uniform"):
+        if (pm.get("values"), pm.get("size")) != want or not (world == 1 or args.workload in ("uniform", "big")):
             traffic_refused = "no PMC passes of this workload"
         elif pm.get("build_id") != L.build_id():
             traffic_refused = (f"PMC passes taken with build {pm.get('build_id')}, this run uses {L.build_id()}")
-        elif args.workload == "uniform" and not got_names <= set(names[dom_key]):
+        elif args.workload in ("uniform", "big") and not got_names <= set(names[dom_key]):
             traffic_refused = f"PMC kernel {sorted(got_names)} not among this run's {names[dom_key]}"
         elif args.workload == "mixed" and got_names != set(names[dom_key]):
             traffic_refused = f"PMC kernels {sorted(got_names)} differ from this run's {names[dom_key]}"
@@ -671,7 +681,7 @@ def main() -> None:
     per_gpu = gather_ranks(raw * args.steps / mine / GIB)
     copy_gbs = copy_bandwidth(batch, stream)
     line = {
-        "metric": METRIC,
+        "metric": METRIC if args.workload != "big" else METRIC_BIG,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -686,10 +696,13 @@ def main() -> None:
         "config": {
             "workload": (f"{n} x {size} B values per GPU: CompressorLZ4 frame compress + frame decompress (round trip)"
                          if args.workload == "uniform" else
+                         f"KingDB's default part size (util/options.h:171-172): {n} x {size} B parts per GPU, "
+                         f"byU32 blocks (lz4.cc:673-676): CompressorLZ4 frame compress + frame decompress (round trip)"
+                         if args.workload == "big" else
                          f"configs[3] mixed batch, {n} values on rank 0 (by count 90% 100 B / 9% 4 KiB / 1% 64 KiB "
                          f"parts, {args.values * world} values byte-balanced over {world} GPU(s)): frame compress + "
                          f"frame decompress (round trip)"),
-            "values_per_gpu": n, "value_bytes": size if args.workload == "uniform" else "mixed",
+            "values_per_gpu": n, "value_bytes": size if args.workload in ("uniform", "big") else "mixed",
             "raw_bytes_per_gpu": int(raw),
             "parallelism": f"dp{world} (independent shards, no collective)",
             "ratio": round(frames / raw, 4),
@@ -714,11 +727,12 @@ def main() -> None:
                       "statuses and lengths only (poisoned before the timed steps)")
     if not args.no_host_inclusive and args.workload == "uniform" and world == 1:
         line["host_inclusive"] = host_inclusive(batch, n, size, args)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "uniform":
-        ncpu = min(n, 131072)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("uniform", "big"):
+        ncpu = min(n, 131072, max(1, (1 << 30) // size))   # at most 1 GiB of the batch
         sample = batch.src.download(ncpu * size)
         line["cpu_baseline"] = cpu_baseline(sample, size, args.cpu_seconds)
-        line["configs0_compressor_100b"] = compressor_calls_100b()
+        if args.workload == "uniform":
+            line["configs0_compressor_100b"] = compressor_calls_100b()
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "mixed":
         # a prefix of the same batch, about 512 MiB of raw bytes
         lens = batch.sizes

@@ -58,6 +58,11 @@ int kdb_lz4_warmup(void);
  * instances that exited served, *alive = 1 while one is resident.  All 0 when
  * the service was never used on the device.  No HIP call. */
 int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint32_t* alive);
+/* The same device's services' protocol counters (diagnostics; added when the
+ * waves exit): polls made, requests taken from their posts (arguments and
+ * input read with the doorbells, no second PCIe round trip), and decode
+ * results answered by a reply record ahead of the done word (service.h). */
+int kdb_lz4_service_counters(int device, uint32_t* polls, uint32_t* from_post, uint32_t* replied);
 /* The kernels (rocprof names, ';'-separated) that the calling thread's last
  * compress or decompress batch queued.  No HIP call. */
 int kdb_lz4_last_kernels(char* buf, uint64_t cap);

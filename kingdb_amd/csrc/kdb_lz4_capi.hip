@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "../../include/kdb_lz4.h"
@@ -250,6 +251,14 @@ Service* service_of(int dev, int kind, int wave) {
   s->life_ticks = 20ull * (uint64_t)rate_khz;    // 20 ms, then a fresh instance (bounds how long a
                                                   // batch launch can wait behind the wave for a slot)
   for (int i = (int)kSvcSlots - 1; i >= 0; i--) s->free_slots.push_back(i);
+  // A/B knobs of the protocol (service.h): KDB_LZ4_SVC_POST=0 has the wave
+  // fetch every request, KDB_LZ4_SVC_REPLY=0 answer every one by its done word
+  const char* po = getenv("KDB_LZ4_SVC_POST");
+  const char* re = getenv("KDB_LZ4_SVC_REPLY");
+  s->box->no_post = po && *po == '0';
+  s->box->no_reply = re && *re == '0';
+  const char* pp = getenv("KDB_LZ4_SVC_PIPE");   // KDB_LZ4_SVC_PIPE=0: one poll in flight
+  s->box->no_pipe = pp && *pp == '0';
   static bool registered = false;
   if (!registered) {
     registered = true;
@@ -346,7 +355,10 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
     p.csize = in_len;
     p.osize = cap;
     p.target = (uint32_t)target;
-    if (in_len) memcpy(in_len <= kSvcInline ? p.data : sl.in, source, in_len);
+    if (in_len) memcpy(in_len <= kSvcPostInline ? p.data : sl.in, source, in_len);
+    uint32_t w[32];
+    memcpy(w, &p, sizeof(w));
+    p.sum = svc_sum_host(w, 1, 29);
     __atomic_store_n(&p.tag1, want, __ATOMIC_RELEASE);
     __atomic_store_n(&p.tag0, want, __ATOMIC_RELEASE);
   } else {
@@ -361,13 +373,37 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   s->ensure_running();
   const auto t0 = std::chrono::steady_clock::now();
   uint64_t done = 0;
+  // a short decode result comes back in the slot's reply (service.h), ahead of
+  // the done word: taken when both tags are this request's and the checksum
+  // of its 108 data bytes matches
+  SvcReply* rp =
+      (uint32_t)k < kSvcPostSlots && kind == kSvcDecode && !s->box->no_reply ? &s->box->reply[k] : nullptr;
   for (uint32_t spins = 1;; spins++) {
+    if (rp && __atomic_load_n(&rp->tag0, __ATOMIC_ACQUIRE) == want) {
+      SvcReply r;
+      memcpy(&r, rp, sizeof(r));
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      uint32_t w[27];
+      memcpy(w, r.data, sizeof(w));
+      const uint32_t sum = svc_sum_host(w, 0, 27);
+      if (r.tag0 == want && r.tag1 == want && r.sum == sum && r.rc >= 0 && r.rc <= (int32_t)kSvcInline &&
+          r.rc <= (int32_t)cap) {
+        *ret = r.rc;
+        if (r.rc > 0) memcpy(dest, r.data, (size_t)r.rc);
+        return true;
+      }
+    }
     done = __atomic_load_n(&s->box->done[k], __ATOMIC_ACQUIRE);
-    if ((uint32_t)(done >> 32) == want) break;
+    // answered in the reply record (its bytes may still be on their way): keep
+    // reading the reply
+    if ((uint32_t)(done >> 32) == want && !(rp && ((uint32_t)done & 0xC0000000u) == kSvcReplied)) break;
     __builtin_ia32_pause();
     if ((spins & 1023u) == 0) {
       const auto waited = std::chrono::steady_clock::now() - t0;
       if (waited > std::chrono::microseconds(200)) s->ensure_running();   // it had just left: once more
+      // past half a millisecond (a busy device, a service being relaunched)
+      // the thread stops burning its core: it sleeps between checks
+      if (waited > std::chrono::microseconds(500)) std::this_thread::sleep_for(std::chrono::microseconds(20));
       if (waited > std::chrono::seconds(1)) {
         // no answer (the device busy past a second?): this thread gives the
         // slot up for good (the wave may still write it) and launches
@@ -399,7 +435,24 @@ int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint
       if (!s || !s->ok) continue;
       *launches += __atomic_load_n(&s->box->launches, __ATOMIC_ACQUIRE);
       *served += __atomic_load_n(&s->box->served, __ATOMIC_ACQUIRE);
-      *alive += __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE);
+      *alive += __atomic_load_n(&s->box->alive, __ATOMIC_ACQUIRE) != 0u ? 1u : 0u;   // (a generation)
+    }
+  return KDB_LZ4_OK;
+}
+
+int kdb_lz4_service_counters(int device, uint32_t* polls, uint32_t* from_post, uint32_t* replied) {
+  if (!polls || !from_post || !replied || device < 0) return KDB_LZ4_EINVAL;
+  *polls = *from_post = *replied = 0;
+  std::lock_guard<std::mutex> l(g_svc_mu);
+  const std::vector<Service*>& v = services();
+  for (int kind = 0; kind < 2; kind++)
+    for (int w = 0; w < kSvcWavesMax; w++) {
+      const size_t at = svc_index(device, kind, w);
+      const Service* s = at < v.size() ? v[at] : nullptr;
+      if (!s || !s->ok) continue;
+      *polls += __atomic_load_n(&s->box->polls, __ATOMIC_ACQUIRE);
+      *from_post += __atomic_load_n(&s->box->inline_served, __ATOMIC_ACQUIRE);
+      *replied += __atomic_load_n(&s->box->replied, __ATOMIC_ACQUIRE);
     }
   return KDB_LZ4_OK;
 }
@@ -539,7 +592,36 @@ int kdb_lz4_stream_create(void** stream) {
 }
 int kdb_lz4_stream_destroy(void* stream) { return hip_status(hipStreamDestroy((hipStream_t)stream)); }
 int kdb_lz4_stream_sync(void* stream) { return hip_status(hipStreamSynchronize((hipStream_t)stream)); }
-int kdb_lz4_device_sync(void) { return hip_status(hipDeviceSynchronize()); }
+// Waits for the calling thread's device.  A resident service wave (service.h)
+// counts as work in flight for hipDeviceSynchronize and would hold it for up
+// to its idle time (2 ms) or lifetime (20 ms): the device's services are told
+// to leave first (each serves what is already rung), and callers that ring
+// meanwhile wait on the service's lock, then relaunch it after the sync.
+int kdb_lz4_device_sync(void) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_status(e);
+  std::vector<Service*> held;
+  {
+    std::lock_guard<std::mutex> l(g_svc_mu);
+    for (int kind = 0; kind < 2; kind++)
+      for (int w = 0; w < kSvcWavesMax; w++) {
+        const size_t at = svc_index(dev, kind, w);
+        Service* s = at < services().size() ? services()[at] : nullptr;
+        if (s && s->ok) held.push_back(s);
+      }
+  }
+  for (Service* s : held) {
+    s->mu.lock();
+    __atomic_store_n(&s->box->stop, 1u, __ATOMIC_SEQ_CST);
+  }
+  e = hipDeviceSynchronize();
+  for (Service* s : held) {
+    __atomic_store_n(&s->box->stop, 0u, __ATOMIC_SEQ_CST);
+    s->mu.unlock();
+  }
+  return hip_status(e);
+}
 int kdb_lz4_event_create(void** event) {
   return event ? hip_status(hipEventCreate((hipEvent_t*)event)) : KDB_LZ4_EINVAL;
 }

@@ -171,6 +171,13 @@ struct Table12 {
   }
 };
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
+// The off-lane addresses of the exchanges (Table12/16/32::xchg) rely on the
+// hardware dropping LDS accesses past the kernel's allocation: they start at
+// 0x10000 past the table's base, so every kernel that uses these tables must
+// allocate less LDS than that (gfx950 allows up to 160 KiB per workgroup).
+// Checked statically for the fixed layouts below and at launch for the
+// dynamically sized one (launch_one, the 4-8 KiB class).
+constexpr uint32_t kOffLaneLds = 0x10000u;
 
 // byU16 table, 8192 x u16 (values up to 65 546 bytes; positions < 65 536).
 struct Table16 {
@@ -1081,7 +1088,8 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
   __syncthreads();
   Table12 tab;
   // the value staged at LDS [0, S) by svc_loop
-  svc_loop(box, gen, idle_ticks, life_ticks, smem_s, kSmallMax, [&](uint32_t sidx, const SvcArgs& a) -> int {
+  svc_loop(box, gen, idle_ticks, life_ticks, smem_s, kSmallMax,
+           [&](uint32_t sidx, const SvcArgs& a, const uint8_t**) -> int {
     const uint32_t S = a.csize, cap = a.osize;
     int rc = (int)kUnsupported;
     if (S <= kSmallMax && cap <= kSvcOutBytes) {
@@ -1105,6 +1113,9 @@ hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint32_t gen, ui
   return hipGetLastError();
 }
 
+static_assert(kTable12Bytes + kSmallMax <= kOffLaneLds, "Table12 kernels: off lanes must address past the LDS");
+static_assert(kTableBytes + kMidLdsMax <= kOffLaneLds, "the LDS-staged class: off lanes must address past the LDS");
+static_assert(4096u * 4u <= kOffLaneLds, "Table32 kernels: off lanes must address past the LDS");
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
   // 16 KiB: 10 per CU
@@ -1274,6 +1285,7 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
                              int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0,
                              uint32_t guide = 0) {
   auto kern = lz4_compress_kernel<F, Sm, Em>;
+  if (lds + (Sm ? kTable12Bytes + kSmallMax : 16u) > kOffLaneLds) return hipErrorInvalidValue;   // see kOffLaneLds
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
   uint32_t* work = nullptr;
   hipError_t e = launch_counter(st, n, grid, &work);

@@ -977,16 +977,19 @@ __global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uin
   constexpr uint32_t s_in_cap = (kSvcMaxIn + 32u + 15u) & ~15u;   // small_decode_loop's layout
   uint8_t* s_in = smem;
   uint8_t* s_out = smem + s_in_cap;
+  const bool reply_on = __hip_atomic_load(&box->no_reply, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u;
   // the block staged at s_in (head 0) by svc_loop
-  svc_loop(box, gen, idle_ticks, life_ticks, s_in, kSvcMaxIn, [&](uint32_t sidx, const SvcArgs& a) -> int {
+  svc_loop(box, gen, idle_ticks, life_ticks, s_in, kSvcMaxIn,
+           [&](uint32_t sidx, const SvcArgs& a, const uint8_t** res) -> int {
     const int csize = (int)a.csize, osize = (int)a.osize, tgt = (int)a.target;
     int rc = (int)kUnsupported;
     if (csize >= 0 && osize >= 0 && (uint32_t)csize <= kSvcMaxIn && (uint32_t)osize <= kSvcMaxOut) {
       if (lane < 16u) s_in[(uint32_t)csize + lane] = 0;   // OOB bytes read as 0
       __syncthreads();
       rc = decode_block(s_in, 0u, csize, s_out, osize, tgt);
-      if (rc > 0) flush_lds_to_global(box->slot[sidx].out, s_out, 0, (uint32_t)rc);
-      __syncthreads();
+      // a short result goes back in the slot's reply (svc_loop), the rest here
+      if (rc > 0 && !(reply_on && svc_replies(sidx, rc))) flush_lds_to_global(box->slot[sidx].out, s_out, 0, (uint32_t)rc);
+      *res = s_out;   // the reply reads it before the next request's staging
     }
     return rc;
   });

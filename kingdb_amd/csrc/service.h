@@ -19,7 +19,7 @@
 // for is PCIe round trips (round 5):
 //  * each poll (relaxed system-scope loads, which bypass the caches) also reads the first kSvcPostSlots slots' POSTS: a 128-byte
 //    record per slot holding the request's arguments and, for inputs up to
-//    kSvcInline bytes (a 100-byte value, or its ~60-byte block), the input
+//    kSvcPostInline bytes (a 100-byte value, or its ~60-byte block), the input
 //    itself.  The host writes the post, then its two tags (one per 64-byte
 //    line: tag1 at the end of line 1, then tag0 at the start of line 0), then
 //    the doorbell.  A 64-byte line is read as one unit, so a line whose tag
@@ -54,7 +54,8 @@ constexpr uint32_t kSvcMaxIn = kSvcMaxOut + kSvcMaxOut / 255u + 24u;
 constexpr uint32_t kSvcInBytes = (kSvcMaxIn + 64u + 15u) & ~15u;
 constexpr uint32_t kSvcOutBytes = kSvcMaxOut + 64u;
 constexpr uint32_t kSvcPostSlots = 16;       // slots whose posts every poll reads (2 KiB)
-constexpr uint32_t kSvcInline = 108;         // input bytes a post carries
+constexpr uint32_t kSvcInline = 108;         // result bytes a reply carries
+constexpr uint32_t kSvcPostInline = 104;     // input bytes a post carries
 
 // A request's arguments: LZ4_decompress_safe_partial's (csize, osize, target)
 // or LZ4_compress_limitedOutput's (input bytes, output capacity).
@@ -63,14 +64,53 @@ struct SvcArgs {
 };
 
 // A slot's post (slots < kSvcPostSlots): line 0 = tag0, the arguments and
-// input bytes [0, 48); line 1 = input bytes [48, 108) and tag1.
+// input bytes [0, 48); line 1 = input bytes [48, 104), a checksum of dwords
+// 1-29 (the arguments and the input: svc_weight) and tag1.  The tags say
+// which request the lines belong to; the checksum guards against a line the
+// wave read in pieces across the host's write (measured: a post taken on
+// tags alone decoded wrong bytes once in some 10^4 calls).
 struct SvcPost {
   uint32_t tag0;
   uint32_t csize, osize, target;
-  uint8_t data[kSvcInline];
+  uint8_t data[kSvcPostInline];
+  uint32_t sum;
   uint32_t tag1;
 };
 static_assert(sizeof(SvcPost) == 128, "two 64-byte lines");
+
+// A slot's reply (decode service, slots < kSvcPostSlots, results up to
+// kSvcInline bytes): line 0 = tag0, the return value, a checksum of the 108
+// data bytes, then data[0, 48); line 1 = data[48, 108) and tag1.  Written by
+// one store instruction (8 lanes x 16 bytes), with no release: the host takes
+// the result from it when both tags are the request's number and the
+// checksum matches (svc_weight, kdb_lz4_capi.hip), which spares the
+// wait for the result's write to be acknowledged before the done word; the
+// done word (relaxed) only says kSvcReplied, and a host that reads a reply
+// whose bytes are not all there yet reads it again.
+struct SvcReply {
+  uint32_t tag0;
+  int32_t rc;
+  uint32_t sum, pad;
+  uint8_t data[kSvcInline];
+  uint32_t tag1;
+};
+static_assert(sizeof(SvcReply) == 128, "two 64-byte lines");
+// Whether slot sidx's result of return value rc goes back in a reply (the
+// serve callback then leaves slot.out unwritten); its done word then holds
+// kSvcReplied | rc, a value no return code takes (results are < 2^30; error
+// codes are negative).
+constexpr uint32_t kSvcReplied = 0x40000000u;
+__host__ __device__ inline bool svc_replies(uint32_t sidx, int rc) {
+  return sidx < kSvcPostSlots && rc >= 0 && rc <= (int)kSvcInline;
+}
+// the checksums: the sum of dword i x (2 i + 1) x 0x9E3779B1 (mod 2^32) over
+// a record's dwords: any one dword that differs changes it (odd factors)
+__host__ __device__ inline uint32_t svc_weight(uint32_t i) { return (2u * i + 1u) * 0x9E3779B1u; }
+__host__ inline uint32_t svc_sum_host(const uint32_t* w, uint32_t first, uint32_t n) {
+  uint32_t s = 0;
+  for (uint32_t i = first; i < first + n; i++) s += w[i] * svc_weight(i);
+  return s;
+}
 
 struct SvcSlot {
   uint8_t in[kSvcInBytes];         // the block / value (16-byte aligned), when not in the post
@@ -87,8 +127,12 @@ struct SvcBox {
   uint32_t active;                 // host: 1 + the highest slot leased (how many posts a poll reads)
   uint32_t gen;                    // host: the last generation launched
   uint32_t polls, inline_served;   // device: counters (diagnostics)
-  uint32_t pad[56];
+  uint32_t replied;                // device: requests answered by a reply (diagnostics)
+  uint32_t no_post, no_reply;      // host: the wave ignores the posts / never replies (A/B knobs)
+  uint32_t no_pipe;                // host: one poll in flight instead of two (A/B knob)
+  uint32_t pad[52];
   SvcPost post[kSvcPostSlots];     // 128-byte aligned (offset 2048)
+  SvcReply reply[kSvcPostSlots];
   SvcSlot slot[kSvcSlots];
 };
 static_assert(offsetof(SvcBox, post) % 128 == 0 && offsetof(SvcBox, slot) % 16 == 0, "mailbox layout");
@@ -107,7 +151,7 @@ typedef uint32_t svc_u32x4 __attribute__((ext_vector_type(4)));
 // posts of slots 0-7, resp. 8-15).  Every load is relaxed at system scope
 // (sc0 sc1: past the caches).
 struct SvcPoll {
-  uint32_t r, act;
+  uint32_t r, act, stop;
   svc_u32x4 p0, p1;
 };
 __device__ __forceinline__ SvcPoll svc_poll(SvcBox* box, uint32_t act) {
@@ -115,7 +159,8 @@ __device__ __forceinline__ SvcPoll svc_poll(SvcBox* box, uint32_t act) {
   SvcPoll q;
   q.r = svc_relaxed(&box->req[lane]);
   q.act = svc_relaxed(&box->active);
-  // the same four loads every poll (so the wait for the older poll is a
+  q.stop = svc_relaxed(&box->stop);
+  // the same five loads every poll (so the wait for the older poll is a
   // static count); posts past the leased slots lie past the buffer's range
   // and read as 0 without touching memory.  Cache policy 17 = sc0 | sc1
   // (system scope) on gfx950.
@@ -149,7 +194,7 @@ __device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t
   const uint32_t n = a.csize < max_in ? a.csize : max_in;
   const uint32_t chunks = (n + 15u) >> 4;
   uint4* l4 = reinterpret_cast<uint4*>(lds);
-  if (posted && a.csize <= kSvcInline) {         // the input is in the post
+  if (posted && a.csize <= kSvcPostInline) {     // the input is in the post
     if (lane < chunks) l4[lane] = pc;
     return a;
   }
@@ -180,21 +225,61 @@ __device__ __forceinline__ bool svc_from_post(const SvcPoll& q, uint32_t sidx, u
                  w = hi ? q.p1.w : q.p0.w;
   const uint32_t tag0 = readlane(x, b), tag1 = readlane(w, b + 7u);
   if (tag0 != want || tag1 != want) return false;
+  // the checksum over dwords 1-29 (dword d = 4 (lane - b) + component)
+  uint32_t part = 0;
+  if (lane >= b && lane < b + 8u) {
+    const uint32_t d0 = 4u * (lane - b);
+    part = (d0 >= 1u ? x * svc_weight(d0) : 0u) + y * svc_weight(d0 + 1u) + (d0 + 2u <= 29u ? z * svc_weight(d0 + 2u) : 0u) +
+           (d0 + 3u <= 29u ? w * svc_weight(d0 + 3u) : 0u);
+  }
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 8u; ++j) sum += readlane(part, b + j);
+  if (sum != readlane(z, b + 7u)) return false;
   a->csize = readlane(y, b);
   a->osize = readlane(z, b);
   a->target = readlane(w, b);
   a->pad = 0;
-  if (a->csize > kSvcInline) return false;        // the input is in the slot: fetch it
+  if (a->csize > kSvcPostInline) return false;    // the input is in the slot: fetch it
   // lanes b+1 .. b+7 hold post bytes [16, 128): input bytes [0, 112)
   if (lane > b && lane < b + 8u) reinterpret_cast<uint4*>(lds)[lane - b - 1u] = make_uint4(x, y, z, w);
   return true;
 }
 
+// (svc_replies) Writes slot sidx's reply (request `want`, return value rc, result bytes at
+// LDS `res`, 16-byte aligned, readable for 112 bytes).
+__device__ __forceinline__ void svc_write_reply(SvcBox* box, uint32_t sidx, uint32_t want, int rc,
+                                                const uint8_t* res) {
+  const uint32_t lane = lane_id();
+  // lane j (0..7) holds reply bytes [16 j, 16 j + 16); data dword i sits at
+  // reply byte 16 + 4 i
+  svc_u32x4 d = {0u, 0u, 0u, 0u};
+  if (lane >= 1u && lane < 8u) {
+    const uint4 x = reinterpret_cast<const uint4*>(res)[lane - 1u];
+    d = svc_u32x4{x.x, x.y, x.z, x.w};
+  }
+  uint32_t part = 0;
+  if (lane >= 1u && lane < 8u) {
+    const uint32_t i0 = 4u * (lane - 1u);
+    part = d.x * svc_weight(i0) + d.y * svc_weight(i0 + 1u) + d.z * svc_weight(i0 + 2u);
+    if (lane < 7u) part += d.w * svc_weight(i0 + 3u);   // lane 7's last dword is tag1
+  }
+  uint32_t sum = 0;
+#pragma unroll
+  for (uint32_t j = 1; j < 8u; ++j) sum += readlane(part, j);
+  if (lane == 0u) d = svc_u32x4{want, (uint32_t)rc, sum, 0u};
+  if (lane == 7u) d.w = want;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(&box->reply[sidx], 0, 128, 0x00020000);
+  // sc0 sc1: straight to system memory
+  __builtin_amdgcn_raw_buffer_store_b128(d, rs, lane < 8u ? (int)(16u * lane) : (int)0x80000000, 0, 17);
+}
+
 // The service loop shared by both kinds: polls, takes each
-// pending slot's request (from its post, or fetched), runs serve(sidx, args)
-// -- the input at lds[0, csize), returning the return word after writing the
-// result bytes to box->slot[sidx].out -- then publishes (request << 32 | rc)
-// in the slot's done word.  Every wave reaches an exit: idle_ticks without a
+// pending slot's request (from its post, or fetched), runs serve(sidx, args,
+// &res) -- the input at lds[0, csize), returning the return word after
+// writing the result bytes to box->slot[sidx].out (and setting res to the
+// result's LDS copy, if it has one) -- then writes the reply (short results
+// in LDS) and publishes (request << 32 | rc) in the slot's done word.  Every wave reaches an exit: idle_ticks without a
 // request, life_ticks in all, or the host's stop.
 template <class Serve>
 __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
@@ -204,8 +289,9 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
   uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
   const uint64_t t0 = wall_clock64();
   uint64_t t_last = t0;
-  uint32_t served = 0, polls = 0, inl = 0;
+  uint32_t served = 0, polls = 0, inl = 0, rep = 0;
   uint32_t act = kSvcPostSlots;
+  const bool post_on = svc_relaxed(&box->no_post) == 0u, reply_on = svc_relaxed(&box->no_reply) == 0u;
   auto serve_pending = [&](uint64_t pend, const SvcPoll& q) {
 #pragma unroll 1
     while (pend) {
@@ -213,7 +299,7 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
       pend &= pend - 1u;
       const uint32_t want = readlane(q.r, sidx);
       SvcArgs a;
-      if (svc_from_post(q, sidx, want, lds, &a)) {
+      if (post_on && svc_from_post(q, sidx, want, lds, &a)) {
         inl++;
       } else {
         // the doorbell's writes before the fetch's plain loads (a relaxed
@@ -221,33 +307,39 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         a = svc_fetch(box, sidx, lds, max_in);
       }
-      const int rc = serve(sidx, a);
-      if (lane == 0)   // after the bytes: the request and its return value, one store
+      const uint8_t* res = nullptr;
+      const int rc = serve(sidx, a, &res);
+      if (res && reply_on && svc_replies(sidx, rc)) {
+        // the reply carries the result; the done word only says so (kSvcReplied
+        // | rc), relaxed: no wait for any earlier write to be acknowledged
+        svc_write_reply(box, sidx, want, rc, res);
+        if (lane == 0)
+          __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (kSvcReplied | (uint32_t)rc),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        rep++;
+      } else if (lane == 0) {   // after the bytes: the request and its return value, one store
         __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       if (lane == sidx) seen = want;
       served++;
     }
   };
-  // One poll in flight at a time: a second one, issued while the first is
-  // looked at, would be waited for by the release of every request served
-  // (loads and stores share one in-order counter), costing more than it saves.
-#pragma unroll 1
-  for (;;) {
-    const SvcPoll q = svc_poll(box, act);
+  // true when the wave leaves
+  auto look = [&](const SvcPoll& q) -> bool {
     polls++;
     act = uni(q.act);
     const uint64_t pend = ballot(q.r != seen);
     if (pend) {
       serve_pending(pend, q);
       t_last = wall_clock64();
-      continue;
+      return false;
     }
     const uint64_t now = wall_clock64();
-    const bool stop = svc_relaxed(&box->stop) != 0u, old = now - t0 > life_ticks;
+    const bool stop = uni(q.stop) != 0u, old = now - t0 > life_ticks;
     if (!(stop || old || now - t_last > idle_ticks)) {
       __builtin_amdgcn_s_sleep(1);
-      continue;
+      return false;
     }
     // leave: clear alive (when it is still this instance's), then look at
     // the doorbells once more.  A caller that rang before it read alive sees
@@ -259,17 +351,43 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     const SvcPoll q2 = svc_poll(box, act);
     const uint64_t pend2 = ballot(q2.r != seen);
-    if (pend2 == 0) break;
+    if (pend2 == 0) return true;
     serve_pending(pend2, q2);
-    if (stop || old) break;
+    if (stop || old) return true;
     if (lane == 0 && svc_relaxed(&box->alive) == 0u) svc_store(&box->alive, gen);
     t_last = wall_clock64();
+    return false;
+  };
+  if (svc_relaxed(&box->no_pipe) != 0u) {
+    // one poll in flight at a time
+#pragma unroll 1
+    for (;;) {
+      const SvcPoll q = svc_poll(box, act);
+      if (look(q)) break;
+    }
+  } else {
+    // Two polls in flight, half a read latency apart: each is looked at
+    // while the next one travels, so a doorbell is seen about half a latency
+    // sooner.  Every poll's state (stop included) travels with it, so a look
+    // waits for nothing younger.  (A request answered by its done word waits,
+    // at its release, for the poll in flight too.)  Unrolled by two so that
+    // no poll's registers are copied while its loads are still filling them.
+    SvcPoll qa = svc_poll(box, act);
+    __builtin_amdgcn_s_sleep(16);   // ~1 000 cycles: the stagger
+#pragma unroll 1
+    for (;;) {
+      const SvcPoll qb = svc_poll(box, act);
+      if (look(qa)) break;
+      qa = svc_poll(box, act);
+      if (look(qb)) break;
+    }
   }
   if (lane == 0) {
     __hip_atomic_store(&box->served, svc_relaxed(&box->served) + served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&box->polls, svc_relaxed(&box->polls) + polls, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&box->inline_served, svc_relaxed(&box->inline_served) + inl, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->replied, svc_relaxed(&box->replied) + rep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

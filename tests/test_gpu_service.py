@@ -128,3 +128,52 @@ def test_service_off_is_the_launch_path(gpu, orc):
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, KDB_LZ4_SERVICE="0"))
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def _counters(dev=0):
+    from kingdb_amd import _lib
+    a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    assert _lib.load().kdb_lz4_service_counters(dev, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
+    return a.value, b.value, c.value
+
+
+def test_service_posts_and_replies(gpu, orc):
+    """Round 5's protocol (service.h): a request whose input fits its slot's
+    post (<= 108 bytes) is taken from the poll itself, and a decode result of
+    <= 108 bytes comes back in a reply record ahead of the done word.  Both
+    paths must be the ones that ran (the counters, summed as waves exit), and
+    give the oracle's bytes -- short values, values at the 108-byte edges,
+    longer ones (fetched as before), and 40 threads at once, so that slots
+    past the 16 posted ones take the fetch path beside them."""
+    pool = oracle.g1_pool(orc)
+    rng = random.Random(5)
+    vals = oracle.g1_values(pool, 100, 200) + [b"", b"z", b"a" * 13]
+    vals += [bytes(rng.randrange(256) for _ in range(n)) for n in (92, 93, 107, 108, 109, 110, 120, 200)]
+    vals += [bytes(rng.choice(b"ab") for _ in range(n)) for n in (108, 109, 500, 3000)]
+    time.sleep(0.05)
+    p0, f0, r0 = _counters()
+    for v in vals:
+        b = orc.compress(v)
+        assert gpu.decompress_safe_partial(b, len(v), len(v)) == (len(v), v), len(v)
+        c = gpu.compress_limited_output(v, orc.compress_bound(len(v)))
+        assert c == (len(b), b) or (len(v) == 0 and c[0] == len(b)), len(v)
+    bad = []
+
+    def worker(t):
+        gpu.set_device(0)
+        r = random.Random(t)
+        for _ in range(100):
+            v = vals[r.randrange(len(vals))]
+            if gpu.decompress_safe_partial(orc.compress(v), len(v), len(v)) != (len(v), v):
+                bad.append((t, len(v)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(40)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not bad, bad[:5]
+    time.sleep(0.05)   # the waves leave (2 ms idle) and add their counters
+    p1, f1, r1 = _counters()
+    short = sum(1 for v in vals if len(v) <= 108)
+    assert f1 - f0 >= short and r1 - r0 >= short // 2, (p1 - p0, f1 - f0, r1 - r0, short)
