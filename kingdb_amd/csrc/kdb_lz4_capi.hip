@@ -144,7 +144,7 @@ inline Meta read_meta(const uint8_t* p) {
 }
 
 // ---- the resident services (service.h): per device and process, up to
-// KDB_LZ4_SERVICE_WAVES (default 4) waves for per-call decodes and as many for
+// KDB_LZ4_SERVICE_WAVES (default 8, at most 16) waves for per-call decodes and as many for
 // per-call compressions, each with a mailbox and a stream of its own; a
 // calling thread is assigned one of them (round robin) with its slot, so
 // concurrent callers are served side by side.  KDB_LZ4_SERVICE=0 turns it
@@ -159,11 +159,11 @@ bool service_on() {
 }
 
 enum SvcKind { kSvcDecode = 0, kSvcCompress = 1 };
-constexpr int kSvcWavesMax = 8;
+constexpr int kSvcWavesMax = 16;
 int svc_waves() {
   static const int n = [] {
     const char* e = getenv("KDB_LZ4_SERVICE_WAVES");
-    const int v = e && *e ? atoi(e) : 4;
+    const int v = e && *e ? atoi(e) : 8;
     return v < 1 ? 1 : (v > kSvcWavesMax ? kSvcWavesMax : v);
   }();
   return n;

@@ -212,19 +212,41 @@ __device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t
   return a;
 }
 
+// A request's input (csize bytes, known from its post) staged from the slot
+// into LDS: every chunk in flight at once, one round trip.  After an acquire
+// fence, as svc_fetch.
+__device__ __forceinline__ void svc_fetch_input(SvcBox* box, uint32_t sidx, uint8_t* lds, uint32_t csize,
+                                                uint32_t max_in) {
+  const uint32_t lane = lane_id();
+  const uint32_t n = csize < max_in ? csize : max_in;
+  const uint32_t chunks = (n + 15u) >> 4;
+  const uint4* in4 = reinterpret_cast<const uint4*>(box->slot[sidx].in);
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+  constexpr uint32_t kAll = (kSvcInBytes / 16u + 63u) / 64u;
+  uint4 r[kAll];
+#pragma unroll
+  for (uint32_t k = 0; k < kAll; k++)
+    if (lane + 64u * k < chunks) r[k] = in4[lane + 64u * k];
+#pragma unroll
+  for (uint32_t k = 0; k < kAll; k++)
+    if (lane + 64u * k < chunks) l4[lane + 64u * k] = r[k];
+}
+
 // The request of slot sidx (doorbell `want`) taken from poll q when its post
-// is complete: the arguments, and the input staged at lds[0, csize); false
-// when the post is not usable (then svc_fetch).
-__device__ __forceinline__ bool svc_from_post(const SvcPoll& q, uint32_t sidx, uint32_t want, uint8_t* lds,
+// is complete: the arguments, and the input staged at lds[0, csize).  Returns
+// 0 when the post is not usable (then svc_fetch), 1 when the request is
+// complete, 2 when only the arguments are (its input is in the slot: then
+// svc_fetch_input).
+__device__ __forceinline__ int svc_from_post(const SvcPoll& q, uint32_t sidx, uint32_t want, uint8_t* lds,
                                               SvcArgs* a) {
-  if (sidx >= kSvcPostSlots) return false;
+  if (sidx >= kSvcPostSlots) return 0;
   const uint32_t lane = lane_id();
   const uint32_t b = 8u * (sidx & 7u);           // the post's first lane
   const bool hi = sidx >= 8u;
   const uint32_t x = hi ? q.p1.x : q.p0.x, y = hi ? q.p1.y : q.p0.y, z = hi ? q.p1.z : q.p0.z,
                  w = hi ? q.p1.w : q.p0.w;
   const uint32_t tag0 = readlane(x, b), tag1 = readlane(w, b + 7u);
-  if (tag0 != want || tag1 != want) return false;
+  if (tag0 != want || tag1 != want) return 0;
   // the checksum over dwords 1-29 (dword d = 4 (lane - b) + component)
   uint32_t part = 0;
   if (lane >= b && lane < b + 8u) {
@@ -235,15 +257,15 @@ __device__ __forceinline__ bool svc_from_post(const SvcPoll& q, uint32_t sidx, u
   uint32_t sum = 0;
 #pragma unroll
   for (uint32_t j = 0; j < 8u; ++j) sum += readlane(part, b + j);
-  if (sum != readlane(z, b + 7u)) return false;
+  if (sum != readlane(z, b + 7u)) return 0;
   a->csize = readlane(y, b);
   a->osize = readlane(z, b);
   a->target = readlane(w, b);
   a->pad = 0;
-  if (a->csize > kSvcPostInline) return false;    // the input is in the slot: fetch it
+  if (a->csize > kSvcPostInline) return 2;        // the input is in the slot: fetch it
   // lanes b+1 .. b+7 hold post bytes [16, 128): input bytes [0, 112)
   if (lane > b && lane < b + 8u) reinterpret_cast<uint4*>(lds)[lane - b - 1u] = make_uint4(x, y, z, w);
-  return true;
+  return 1;
 }
 
 // (svc_replies) Writes slot sidx's reply (request `want`, return value rc, result bytes at
@@ -299,13 +321,15 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
       pend &= pend - 1u;
       const uint32_t want = readlane(q.r, sidx);
       SvcArgs a;
-      if (post_on && svc_from_post(q, sidx, want, lds, &a)) {
+      const int how = post_on ? svc_from_post(q, sidx, want, lds, &a) : 0;
+      if (how == 1) {
         inl++;
       } else {
         // the doorbell's writes before the fetch's plain loads (a relaxed
         // load of the doorbell + this fence synchronise with its release)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        a = svc_fetch(box, sidx, lds, max_in);
+        if (how == 2) svc_fetch_input(box, sidx, lds, a.csize, max_in);   // the arguments came with the poll
+        else a = svc_fetch(box, sidx, lds, max_in);
       }
       const uint8_t* res = nullptr;
       const int rc = serve(sidx, a, &res);

@@ -66,7 +66,7 @@ for s in "$@"; do
     quick)
       timeout -k 10 300 python bench.py --no-cpu-baseline --no-host-inclusive > "${O}_quick.json" 2> "${O}_quick.err" || fail quick $? "${O}_quick.err"
       line "${O}_quick.json" ;;
-    mixed|put|get)
+    mixed|put|get|big)
       timeout -k 10 500 python bench.py --workload $s > "${O}_$s.json" 2> "${O}_$s.err" || fail $s $? "${O}_$s.err"
       cat "${O}_$s.json" ;;
     prof) prof bench --no-cpu-baseline --no-host-inclusive --steps 5 --warmup 1 ;;
