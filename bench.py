@@ -672,7 +672,9 @@ def main() -> None:
             traffic = got["hbm_bytes_per_launch"]
             traffic_source = {"file": os.path.relpath(pmc, ROOT), "passes": pm.get("passes"),
                               "build_id": pm.get("build_id"),
-                              "scope": pm.get("scope", "the kind's dominant launch")}
+                              "scope": pm.get("scope", "the kind's dominant launch"),
+                              "correction": got.get("correction"),
+                              "traffic_undoubled": got.get("hbm_bytes_per_launch_undoubled")}
     except (OSError, ValueError, KeyError) as e:
         traffic_refused = f"no usable PMC summary ({type(e).__name__})"
 

@@ -338,6 +338,12 @@ Lease lease_of(int dev, int kind) {
 // used (no service, no free slot, no answer within a second -- the caller
 // then launches as before).  *ret = the kernel's return word, the output
 // copied to dest when it is > 0.
+#if KDB_SVC_DEBUG
+thread_local const uint8_t* t_dbg_out = nullptr;
+thread_local uint64_t t_dbg_done = 0;
+thread_local SvcBox* t_dbg_box = nullptr;
+thread_local std::vector<char> t_dbg_last;
+#endif
 bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uint32_t cap, int target, int* ret) {
   if (!service_on()) return false;
   int dev = 0;
@@ -414,6 +420,11 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   }
   *ret = (int32_t)(uint32_t)done;
   if (*ret > 0) memcpy(dest, sl.out, (size_t)*ret);
+#if KDB_SVC_DEBUG
+  t_dbg_out = sl.out;
+  t_dbg_done = done;
+  t_dbg_box = s->box;
+#endif
   return true;
 }
 
@@ -710,11 +721,48 @@ int kdb_lz4_decompress_safe_partial(const char* source, char* dest, int compress
   // the LDS-resident decoder's share (lz4_decompress.hip: output <= its split,
   // block <= that output's bound + a frame header)
   const bool zc = O <= kZeroCopyMax && C <= kZeroCopyMax + kZeroCopyMax / 255u + 24u;
+#if KDB_SVC_DEBUG   // (diagnostic build: every service answer checked against a launch)
+  static thread_local bool t_no_svc = false;
+  if (zc && C <= kSvcMaxIn && O <= kSvcMaxOut && !t_no_svc) {
+    int sret = 0;
+    std::vector<char> mine((size_t)O + 1);
+    if (service_call(kSvcDecode, source, C, mine.data(), O, targetOutputSize, &sret)) {
+      const int r1 = sret == KDB_LZ4_VALUE_UNSUPPORTED ? -1 : sret;
+      t_no_svc = true;
+      const int r2 = kdb_lz4_decompress_safe_partial(source, dest, compressedSize, targetOutputSize, maxDecompressedSize);
+      t_no_svc = false;
+      size_t at = 0;
+      if (r1 == r2 && r2 > 0) while (at < (size_t)r2 && mine[at] == dest[at]) at++;
+      if (r1 != r2 || (r2 > 0 && at != (size_t)r2)) {
+        const Lease ls = lease_of(0, kSvcDecode);
+        const std::vector<char>& last = t_dbg_last;
+        size_t nbad = 0, stale = 0, later = 0;
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        for (size_t j = 0; r2 > 0 && j < (size_t)r2; j++) {
+          nbad += mine[j] != dest[j];
+          stale += mine[j] != dest[j] && j < last.size() && mine[j] == last[j];
+          later += t_dbg_out && (char)t_dbg_out[j] != dest[j];
+        }
+        fprintf(stderr,
+                "SVCDBG slot %d: C %u O %u target %d: service %d launch %d, first diff %zu, %zu bytes differ, %zu "
+                "of them the slot's previous output; after 2 ms the slot differs in %zu; done %llx alive %u served %u "
+                "launches %u overlaps %u running %u\n",
+                ls.slot, C, O, targetOutputSize, r1, r2, at, nbad, stale, later, (unsigned long long)t_dbg_done,
+                t_dbg_box ? t_dbg_box->alive : 0u, t_dbg_box ? t_dbg_box->served : 0u,
+                t_dbg_box ? t_dbg_box->launches : 0u, t_dbg_box ? t_dbg_box->pad[1] : 0u,
+                t_dbg_box ? t_dbg_box->pad[0] : 0u);
+      }
+      if (r2 > 0) t_dbg_last.assign(dest, dest + r2);
+      return r2;
+    }
+  }
+#else
   if (zc && C <= kSvcMaxIn && O <= kSvcMaxOut) {   // the resident decode service (service.h)
     int sret = 0;
     if (service_call(kSvcDecode, source, C, dest, O, targetOutputSize, &sret))
       return sret == KDB_LZ4_VALUE_UNSUPPORTED ? -1 : sret;
   }
+#endif
   if (zc) {                                      // zero-copy: [meta][in][out] in mapped host memory
     const size_t in_at = kMetaBytes, out_at = kMetaBytes + align16((size_t)C + 16);
     if (c.reserve(out_at + align16((size_t)O + 16), 0) != KDB_LZ4_OK) return -1;

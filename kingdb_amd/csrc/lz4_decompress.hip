@@ -192,7 +192,9 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
       if (tst >= 0) {
 #pragma unroll 1
       do {
+#if !KDB_ABL_DEC_NOLIT   // (attribution build: the fast path's literal stores left out -- timing only)
         ((lds_b*)(uintptr_t)(uint32_t)aop)[0] = (uint8_t)v;       // lz4.cc:947 (lanes past lit: not-yet-produced output)
+#endif
         const int nt = slit + 2 + mx;                             // next token's lane (<= 63)
         sq = readlane(v, (uint32_t)nt);
         avip = als + nt;
@@ -205,8 +207,10 @@ __device__ int decode_block(const uint8_t* __restrict__ lds_in, uint32_t in_off,
         // 0) or one longer than a step takes the branch, which for an
         // overlapping match rewrites the whole match (a plain copy may have
         // read bytes of this step before they were written)
+#if !KDB_ABL_DEC_NOMATCH   // (attribution build: the first match step left out -- timing only)
         const uint8_t b0 = ((const lds_b*)(uintptr_t)(uint32_t)aref)[0];
         ((lds_b*)(uintptr_t)(uint32_t)aopl)[0] = b0;
+#endif
         asm volatile("" ::: "memory");
         if (((off - min(mlen, 64)) | (64 - mlen)) < 0) {
           const int steps = unii(mlen);

@@ -54,6 +54,7 @@ constexpr uint32_t kSvcMaxIn = kSvcMaxOut + kSvcMaxOut / 255u + 24u;
 constexpr uint32_t kSvcInBytes = (kSvcMaxIn + 64u + 15u) & ~15u;
 constexpr uint32_t kSvcOutBytes = kSvcMaxOut + 64u;
 constexpr uint32_t kSvcPostSlots = 16;       // slots whose posts every poll reads (2 KiB)
+
 constexpr uint32_t kSvcInline = 108;         // result bytes a reply carries
 constexpr uint32_t kSvcPostInline = 104;     // input bytes a post carries
 
@@ -140,8 +141,20 @@ static_assert(offsetof(SvcBox, post) % 128 == 0 && offsetof(SvcBox, slot) % 16 =
 __device__ __forceinline__ uint32_t svc_relaxed(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Everything this wave wrote before, out to memory: the release fence's L2
+// write-back (buffer_wbl2), then a wait for it written out here.  The
+// compiler's own wait after the write-back is dropped by its waitcnt pass
+// when no load or store is outstanding (it does not count the write-back),
+// and a store that followed then reached the host ahead of the bytes written
+// before it (tests/test_service_isa.py checks every write-back is waited for).
+__device__ __forceinline__ void svc_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) (expcnt, lgkmcnt: no wait)
+}
+// A store the host reads, after every earlier write of this wave.
 __device__ __forceinline__ void svc_store(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+  svc_release();
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 typedef uint32_t svc_u32x4 __attribute__((ext_vector_type(4)));
@@ -310,6 +323,12 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
   // lane i: the last request of slot i served
   uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
   const uint64_t t0 = wall_clock64();
+#if KDB_SVC_DEBUG   // (diagnostic: instances of this box running at once)
+  if (lane == 0) {
+    const uint32_t was = __hip_atomic_fetch_add(&box->pad[0], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (was != 0u) __hip_atomic_fetch_add(&box->pad[1], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#endif
   uint64_t t_last = t0;
   uint32_t served = 0, polls = 0, inl = 0, rep = 0;
   uint32_t act = kSvcPostSlots;
@@ -341,9 +360,13 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
           __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (kSvcReplied | (uint32_t)rc),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         rep++;
-      } else if (lane == 0) {   // after the bytes: the request and its return value, one store
-        __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELEASE,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        // after the bytes (plain stores, which may sit dirty in L2): the
+        // request and its return value, one store
+        svc_release();
+        if (lane == 0)
+          __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
       }
       if (lane == sidx) seen = want;
       served++;
@@ -406,12 +429,16 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
       if (look(qb)) break;
     }
   }
-  if (lane == 0) {
-    __hip_atomic_store(&box->served, svc_relaxed(&box->served) + served, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&box->polls, svc_relaxed(&box->polls) + polls, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&box->inline_served, svc_relaxed(&box->inline_served) + inl, __ATOMIC_RELEASE,
+#if KDB_SVC_DEBUG
+  if (lane == 0) __hip_atomic_fetch_sub(&box->pad[0], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+  svc_release();
+  if (lane == 0) {   // (statistics: relaxed)
+    __hip_atomic_store(&box->served, svc_relaxed(&box->served) + served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->polls, svc_relaxed(&box->polls) + polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->inline_served, svc_relaxed(&box->inline_served) + inl, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&box->replied, svc_relaxed(&box->replied) + rep, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->replied, svc_relaxed(&box->replied) + rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

@@ -150,7 +150,14 @@ int main(int argc, char** argv) {
             std::string out;
             kdb::Status s = db.Get(r2, k, &out);
             if (!s.IsOK() || out != v) {
-              if (errors++ < 5) fprintf(stderr, "get %s: %s\n", k.c_str(), s.ToString().c_str());
+              if (errors++ < 5) {
+                size_t at = 0;
+                while (at < out.size() && at < v.size() && out[at] == v[at]) at++;
+                size_t bad = 0;
+                for (size_t j = 0; j < out.size() && j < v.size(); j++) bad += out[j] != v[j];
+                fprintf(stderr, "get %s: %s size %zu got %zu, first diff at %zu (%zu bytes differ)\n", k.c_str(),
+                        s.ToString().c_str(), v.size(), out.size(), at, bad);
+              }
             }
           }
           kdb::MultipartReader mp = db.NewMultipartReader(r2, k);

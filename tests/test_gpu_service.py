@@ -177,3 +177,17 @@ def test_service_posts_and_replies(gpu, orc):
     p1, f1, r1 = _counters()
     short = sum(1 for v in vals if len(v) <= 108)
     assert f1 - f0 >= short and r1 - r0 >= short // 2, (p1 - p0, f1 - f0, r1 - r0, short)
+
+
+@pytest.mark.parametrize("busy", [0, 1])
+def test_service_stress_threads(gpu, busy):
+    """tests/cpp/svc_stress: 8 threads of per-call decodes and compressions of
+    hook_mt-shaped values, each checked against the oracle's blocks; with
+    `busy`, batch compressions run on the device meanwhile and the callers
+    pause past the idle time (waves leave and are relaunched)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "svc_stress")
+    if not os.path.exists(exe):
+        pytest.fail("tests/cpp/svc_stress is not built (make -C tests/cpp)")
+    r = subprocess.run([exe, "8", "300", "7", str(busy)], cwd=ROOT, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, KDB_ORACLE_SO=os.path.join(ROOT, "oracle", "liblz4_oracle.so")))
+    assert r.returncode == 0 and "ok:" in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])

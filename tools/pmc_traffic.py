@@ -62,16 +62,33 @@ def main():
            "passes": [os.path.normpath(fdir), os.path.normpath(wdir)],
            "scope": "sum of the kind's launches in one step" if mixed else "the kind's dominant launch",
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; KiB x 1024; "
-                     "FETCH_SIZE doubled (gfx950 half-count of wide reads, MI355X_MICROARCH.md HBM section)",
+                     "FETCH_SIZE doubled (gfx950 half-count of wide reads, MI355X_MICROARCH.md HBM section) -- "
+                     "exact for wide streaming reads; each kernel's `correction` says whether that holds",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k)
         w = write.get(k)
         rd = None if f is None else 2.0 * f * 1024.0
+        rd1 = None if f is None else f * 1024.0
         wr = None if w is None else w * 1024.0
-        res["kernels"][k] = {"kernel": names.get(k), "fetch_size_kib_raw": f, "write_size_kib_raw": w,
-                             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-                             "hbm_bytes_per_launch": None if rd is None or wr is None else rd + wr}
+        nm = names.get(k) or ""
+        # The guide's x2 is calibrated for wide (16 B per lane) streaming reads only.
+        # The LDS-staged kernels read their inputs that way (register prefetch /
+        # staging of whole 16-byte chunks), so x2 applies.  The in-place compress
+        # classes (big / mixed kernels) also gather 4-byte candidate words and the
+        # ring decoder refills with dword loads: for them the true read bytes lie
+        # between the raw count and twice it, and both are reported.
+        narrow = any(t in nm for t in ("big_kernel", "mixed_kernel", "mixed24_kernel"))
+        res["kernels"][k] = {
+            "kernel": nm, "fetch_size_kib_raw": f, "write_size_kib_raw": w,
+            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+            "hbm_bytes_per_launch": None if rd is None or wr is None else rd + wr,
+            "hbm_bytes_per_launch_undoubled": None if rd1 is None or wr is None else rd1 + wr,
+            "correction": ("FETCH_SIZE x2 applies: every read is a 16 B-per-lane streaming load" if not narrow else
+                           "bounds: the launch mixes 16 B-per-lane streaming loads with 4-byte gathers, for "
+                           "which the guide's x2 is uncalibrated; the true HBM bytes lie between "
+                           "hbm_bytes_per_launch_undoubled and hbm_bytes_per_launch"),
+        }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
