@@ -10,6 +10,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -32,8 +33,9 @@ hipError_t launch_decompress(bool frame, hipStream_t st, const uint8_t* src, con
                              const uint32_t* target, uint32_t* out_len, int32_t* ret);
 hipError_t launch_gen_g1(uint8_t* dst, uint64_t first_piece, uint64_t npieces, uint32_t seed,
                          hipStream_t st);
-hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks);
-hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks,
+hipError_t launch_decode_service(hipStream_t st, const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks,
+                                 uint64_t life_ticks);
+hipError_t launch_compress_service(hipStream_t st, const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks,
                                    uint64_t life_ticks);
 }  // namespace kdb_lz4
 
@@ -172,13 +174,21 @@ int svc_waves() {
 inline size_t svc_index(int dev, int kind, int wave) {
   return ((size_t)dev * 2u + (size_t)kind) * (size_t)kSvcWavesMax + (size_t)wave;
 }
+// The inbox may be a write-combining BAR mapping: its stores leave the core's
+// buffers, in no particular order, at a store fence (a no-op cost on host memory).
+inline void svc_wc_fence() { __builtin_ia32_sfence(); }
 struct Service {
   std::mutex mu;
   int kind = kSvcDecode;
   int wave = 0;
   hipStream_t stream = nullptr;
-  SvcBox* box = nullptr;     // host view (pinned, coherent, mapped)
+  SvcBox* box = nullptr;     // the outbox, host view (pinned, coherent, mapped); also the host's copies
+                             // of req and active
   SvcBox* dbox = nullptr;    // its device address
+  SvcBox* in = nullptr;      // the inbox, host view: device memory through the BAR, or `box` (service.h)
+  SvcBox* din = nullptr;     // its device address
+  bool in_device = false;
+  bool no_reply = false;     // KDB_LZ4_SVC_REPLY=0 (also in the inbox, for the wave)
   uint64_t idle_ticks = 0, life_ticks = 0;
   std::vector<int> free_slots;
   bool ok = false;
@@ -190,8 +200,8 @@ struct Service {
     if (gen == 0u) gen = 1u;
     box->gen = gen;
     __atomic_store_n(&box->alive, gen, __ATOMIC_SEQ_CST);
-    const hipError_t e = kind == kSvcDecode ? launch_decode_service(stream, dbox, gen, idle_ticks, life_ticks)
-                                            : launch_compress_service(stream, dbox, gen, idle_ticks, life_ticks);
+    const hipError_t e = kind == kSvcDecode ? launch_decode_service(stream, din, dbox, gen, idle_ticks, life_ticks)
+                                            : launch_compress_service(stream, din, dbox, gen, idle_ticks, life_ticks);
     if (e != hipSuccess) {
       __atomic_store_n(&box->alive, 0u, __ATOMIC_SEQ_CST);
       return false;
@@ -217,12 +227,64 @@ void stop_services() {
   std::lock_guard<std::mutex> l(g_svc_mu);
   for (Service* s : services()) {
     if (!s || !s->ok) continue;
-    __atomic_store_n(&s->box->stop, 1u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&s->in->stop, 1u, __ATOMIC_SEQ_CST);
+    svc_wc_fence();
     const auto t0 = std::chrono::steady_clock::now();
     while (__atomic_load_n(&s->box->alive, __ATOMIC_SEQ_CST) != 0u &&
            std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(50)) {
     }
+#if KDB_SVC_DEBUG   // (diagnostic build: where a served request's wave time went, in 10 ns ticks)
+    const SvcBox* b = s->box;
+    if (b->served)
+      fprintf(stderr,
+              "SVCDBG kind %d wave %d: served %u polls %u launches %u; per request: fetch %.0f serve %.0f answer "
+              "%.0f ticks; wave time per poll %.1f ticks\n",
+              s->kind, s->wave, b->served, b->polls, b->launches, (double)b->pad[2] / b->served,
+              (double)b->pad[3] / b->served, (double)b->pad[4] / b->served, (double)b->pad[5] / (b->polls + 1));
+#endif
   }
+}
+
+// Whether [p, p + n) lies inside one mapping of this process (/proc/self/maps):
+// a device allocation the CPU can reach through the large BAR is mapped at its
+// device address; one it cannot is not mapped at all.
+bool host_mapped(const void* p, size_t n) {
+  FILE* f = fopen("/proc/self/maps", "r");
+  if (!f) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  unsigned long lo = 0, hi = 0;
+  bool in = false;
+  char line[512];
+  while (!in && fgets(line, sizeof(line), f))
+    if (sscanf(line, "%lx-%lx", &lo, &hi) == 2 && lo <= a && a + n <= hi) in = true;
+  fclose(f);
+  return in;
+}
+// The inbox in fine-grained device memory the host writes through the BAR
+// (service.h), when the device has a large BAR (KDB_LZ4_SVC_INBOX=host keeps
+// it in host memory); nullptr when it cannot be had.
+SvcBox* device_inbox(int dev, hipStream_t st) {
+  const char* e = getenv("KDB_LZ4_SVC_INBOX");
+  if (e && strcmp(e, "host") == 0) return nullptr;
+  int large_bar = 0;
+  if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, dev) != hipSuccess || !large_bar) return nullptr;
+  void* d = nullptr;
+  if (hipExtMallocWithFlags(&d, sizeof(SvcBox), hipDeviceMallocFinegrained) != hipSuccess) return nullptr;
+  SvcBox* b = static_cast<SvcBox*>(d);
+  bool ok = hipMemsetAsync(d, 0, sizeof(SvcBox), st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess &&
+            host_mapped(d, sizeof(SvcBox));
+  if (ok) {   // a canary through the mapping and back
+    __atomic_store_n(&b->pad[0], 0x5A17C0DEu, __ATOMIC_SEQ_CST);
+    svc_wc_fence();
+    ok = __atomic_load_n(&b->pad[0], __ATOMIC_SEQ_CST) == 0x5A17C0DEu;
+    __atomic_store_n(&b->pad[0], 0u, __ATOMIC_SEQ_CST);
+    svc_wc_fence();
+  }
+  if (!ok) {
+    hipFree(d);
+    return nullptr;
+  }
+  return b;
 }
 
 Service* service_of(int dev, int kind, int wave) {
@@ -250,15 +312,23 @@ Service* service_of(int dev, int kind, int wave) {
   s->idle_ticks = idle_us * (uint64_t)rate_khz / 1000u;
   s->life_ticks = 20ull * (uint64_t)rate_khz;    // 20 ms, then a fresh instance (bounds how long a
                                                   // batch launch can wait behind the wave for a slot)
+  s->in = s->box;
+  s->din = s->dbox;
+  if (SvcBox* ib = device_inbox(dev, s->stream)) {
+    s->in = s->din = ib;
+    s->in_device = true;
+  }
   for (int i = (int)kSvcSlots - 1; i >= 0; i--) s->free_slots.push_back(i);
   // A/B knobs of the protocol (service.h): KDB_LZ4_SVC_POST=0 has the wave
   // fetch every request, KDB_LZ4_SVC_REPLY=0 answer every one by its done word
   const char* po = getenv("KDB_LZ4_SVC_POST");
   const char* re = getenv("KDB_LZ4_SVC_REPLY");
-  s->box->no_post = po && *po == '0';
-  s->box->no_reply = re && *re == '0';
+  s->no_reply = re && *re == '0';
+  s->in->no_post = po && *po == '0';
+  s->in->no_reply = s->no_reply;
   const char* pp = getenv("KDB_LZ4_SVC_PIPE");   // KDB_LZ4_SVC_PIPE=0: one poll in flight
-  s->box->no_pipe = pp && *pp == '0';
+  s->in->no_pipe = pp && *pp == '0';
+  svc_wc_fence();
   static bool registered = false;
   if (!registered) {
     registered = true;
@@ -325,8 +395,12 @@ Lease lease_of(int dev, int kind) {
       s->free_slots.pop_back();
       // how many posts the wave's polls read (service.h): the leased slots'
       const uint32_t hi = (uint32_t)got.slot + 1u;
-      if (hi > __atomic_load_n(&s->box->active, __ATOMIC_RELAXED))
-        __atomic_store_n(&s->box->active, std::min(hi, kSvcPostSlots), __ATOMIC_RELEASE);
+      if (hi > __atomic_load_n(&s->box->active, __ATOMIC_RELAXED)) {   // (the host's copy)
+        const uint32_t a = std::min(hi, kSvcPostSlots);
+        __atomic_store_n(&s->box->active, a, __ATOMIC_RELAXED);
+        __atomic_store_n(&s->in->active, a, __ATOMIC_RELEASE);
+        svc_wc_fence();
+      }
     }
   }
   lease.slot[key] = got;
@@ -352,29 +426,40 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   if (ls.slot < 0) return false;
   Service* s = ls.s;
   const int k = ls.slot;
+  SvcSlot& sl_in = s->in->slot[k];
   SvcSlot& sl = s->box->slot[k];
+  // the request number: from the host's copy (the inbox may be device memory,
+  // whose reads cross PCIe)
   const uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
   if ((uint32_t)k < kSvcPostSlots) {
-    // the post: arguments and (up to kSvcInline bytes) the input, then tag1,
-    // then tag0 -- each line's tag after its bytes (service.h)
-    SvcPost& p = s->box->post[k];
+    // the post: arguments and (up to kSvcPostInline bytes) the input, the
+    // checksum and both tags, built here and written whole (service.h)
+    SvcPost p;
+    p.tag0 = p.tag1 = want;
     p.csize = in_len;
     p.osize = cap;
     p.target = (uint32_t)target;
-    if (in_len) memcpy(in_len <= kSvcPostInline ? p.data : sl.in, source, in_len);
+    const bool inl = in_len <= kSvcPostInline;
+    if (inl) {
+      if (in_len) memcpy(p.data, source, in_len);
+      memset(p.data + in_len, 0, kSvcPostInline - in_len);
+    } else {
+      memset(p.data, 0, kSvcPostInline);
+      memcpy(sl_in.in, source, in_len);
+    }
     uint32_t w[32];
     memcpy(w, &p, sizeof(w));
     p.sum = svc_sum_host(w, 1, 29);
-    __atomic_store_n(&p.tag1, want, __ATOMIC_RELEASE);
-    __atomic_store_n(&p.tag0, want, __ATOMIC_RELEASE);
+    memcpy(&s->in->post[k], &p, sizeof(p));
   } else {
-    SvcArgs& a = s->box->args[k];
-    a.csize = in_len;
-    a.osize = cap;
-    a.target = (uint32_t)target;
-    if (in_len) memcpy(sl.in, source, in_len);
+    const SvcArgs a{in_len, cap, (uint32_t)target, 0u};
+    memcpy(&s->in->args[k], &a, sizeof(a));
+    if (in_len) memcpy(sl_in.in, source, in_len);
   }
-  __atomic_store_n(&s->box->req[k], want, __ATOMIC_RELEASE);     // the doorbell, after the arguments
+  svc_wc_fence();                                                 // the request's bytes, then
+  __atomic_store_n(&s->in->req[k], want, __ATOMIC_RELEASE);       // the doorbell
+  __atomic_store_n(&s->box->req[k], want, __ATOMIC_RELAXED);      // (the host's copy; the same word without a BAR)
+  svc_wc_fence();                                                 // on its way now
   __atomic_thread_fence(__ATOMIC_SEQ_CST);                        // ... and before alive is read
   s->ensure_running();
   const auto t0 = std::chrono::steady_clock::now();
@@ -383,7 +468,7 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   // the done word: taken when both tags are this request's and the checksum
   // of its 108 data bytes matches
   SvcReply* rp =
-      (uint32_t)k < kSvcPostSlots && kind == kSvcDecode && !s->box->no_reply ? &s->box->reply[k] : nullptr;
+      (uint32_t)k < kSvcPostSlots && kind == kSvcDecode && !s->no_reply ? &s->box->reply[k] : nullptr;
   for (uint32_t spins = 1;; spins++) {
     if (rp && __atomic_load_n(&rp->tag0, __ATOMIC_ACQUIRE) == want) {
       SvcReply r;
@@ -624,11 +709,13 @@ int kdb_lz4_device_sync(void) {
   }
   for (Service* s : held) {
     s->mu.lock();
-    __atomic_store_n(&s->box->stop, 1u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&s->in->stop, 1u, __ATOMIC_SEQ_CST);
+    svc_wc_fence();
   }
   e = hipDeviceSynchronize();
   for (Service* s : held) {
-    __atomic_store_n(&s->box->stop, 0u, __ATOMIC_SEQ_CST);
+    __atomic_store_n(&s->in->stop, 0u, __ATOMIC_SEQ_CST);
+    svc_wc_fence();
     s->mu.unlock();
   }
   return hip_status(e);

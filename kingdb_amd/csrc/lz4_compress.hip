@@ -1078,7 +1078,7 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
 // as lz4_compress_kernel<false, true> stages it, the block written straight to
 // the slot in host memory.  Every wave reaches an exit: idle_ticks without a
 // request, life_ticks in all, or the host's stop.
-__global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, uint32_t gen, uint64_t idle_ticks,
+__global__ __launch_bounds__(64) void lz4_compress_service_kernel(const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks,
                                                                   uint64_t life_ticks) {
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kTable12Bytes + kSmallMax];   // the kernel's only LDS
   const uint32_t lane = lane_id();
@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
   __syncthreads();
   Table12 tab;
   // the value staged at LDS [0, S) by svc_loop
-  svc_loop(box, gen, idle_ticks, life_ticks, smem_s, kSmallMax,
+  svc_loop(ibox, obox, gen, idle_ticks, life_ticks, smem_s, kSmallMax,
            [&](uint32_t sidx, const SvcArgs& a, const uint8_t**) -> int {
     const uint32_t S = a.csize, cap = a.osize;
     int rc = (int)kUnsupported;
@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
       __syncthreads();
       const uint32_t bound = compress_bound(S);
       LdsSrc ls{smem_s};
-      SvcSlot* sl = &box->slot[sidx];
+      SvcSlot* sl = &obox->slot[sidx];
       rc = cap < bound ? compress_block<false, true>(ls, S, tab, sl->out, (int)cap, (int)cap)
                        : compress_block<false, false>(ls, S, tab, sl->out, (int)bound, (int)cap);
 #pragma unroll
@@ -1107,9 +1107,9 @@ __global__ __launch_bounds__(64) void lz4_compress_service_kernel(SvcBox* box, u
   });
 }
 
-hipError_t launch_compress_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks,
-                                   uint64_t life_ticks) {
-  hipLaunchKernelGGL(lz4_compress_service_kernel, dim3(1), dim3(64), 0, st, box, gen, idle_ticks, life_ticks);
+hipError_t launch_compress_service(hipStream_t st, const SvcBox* ibox, SvcBox* obox, uint32_t gen,
+                                   uint64_t idle_ticks, uint64_t life_ticks) {
+  hipLaunchKernelGGL(lz4_compress_service_kernel, dim3(1), dim3(64), 0, st, ibox, obox, gen, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 

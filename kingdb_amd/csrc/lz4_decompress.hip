@@ -974,16 +974,16 @@ __global__ __launch_bounds__(64) void lz4_decompress_mixed_kernel(
 // exit: after idle_ticks of no requests, after life_ticks in all, or at the
 // host's stop.  Host memory is read and written with system-scope atomics
 // (doorbells, arguments, results) or plain vector loads/stores ordered by them.
-__global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uint32_t gen, uint64_t idle_ticks,
+__global__ __launch_bounds__(64) void lz4_decode_service_kernel(const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks,
                                                                 uint64_t life_ticks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t lane = lane_id();
   constexpr uint32_t s_in_cap = (kSvcMaxIn + 32u + 15u) & ~15u;   // small_decode_loop's layout
   uint8_t* s_in = smem;
   uint8_t* s_out = smem + s_in_cap;
-  const bool reply_on = __hip_atomic_load(&box->no_reply, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u;
+  const bool reply_on = __hip_atomic_load(&ibox->no_reply, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u;
   // the block staged at s_in (head 0) by svc_loop
-  svc_loop(box, gen, idle_ticks, life_ticks, s_in, kSvcMaxIn,
+  svc_loop(ibox, obox, gen, idle_ticks, life_ticks, s_in, kSvcMaxIn,
            [&](uint32_t sidx, const SvcArgs& a, const uint8_t** res) -> int {
     const int csize = (int)a.csize, osize = (int)a.osize, tgt = (int)a.target;
     int rc = (int)kUnsupported;
@@ -992,14 +992,15 @@ __global__ __launch_bounds__(64) void lz4_decode_service_kernel(SvcBox* box, uin
       __syncthreads();
       rc = decode_block(s_in, 0u, csize, s_out, osize, tgt);
       // a short result goes back in the slot's reply (svc_loop), the rest here
-      if (rc > 0 && !(reply_on && svc_replies(sidx, rc))) flush_lds_to_global(box->slot[sidx].out, s_out, 0, (uint32_t)rc);
+      if (rc > 0 && !(reply_on && svc_replies(sidx, rc))) flush_lds_to_global(obox->slot[sidx].out, s_out, 0, (uint32_t)rc);
       *res = s_out;   // the reply reads it before the next request's staging
     }
     return rc;
   });
 }
 
-hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks);
+hipError_t launch_decode_service(hipStream_t st, const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks,
+                                 uint64_t life_ticks);
 
 size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
   // staged block (16 B alignment head + block + 16 zero bytes) | output window
@@ -1113,9 +1114,10 @@ constexpr uint32_t kMixedOutSmall8 = 6144u, kMixedOutSmall4 = 4096u;
 static_assert(kMixedOutSmall4 + kMixedOutSmall4 / 255u + 24u + 32u + 15u + kMixedOutSmall4 + 64u <= 4096u + 4096u + kIMirror,
               "the small pass's staging fits the 4 KiB input ring's LDS");
 
-hipError_t launch_decode_service(hipStream_t st, SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks) {
+hipError_t launch_decode_service(hipStream_t st, const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks,
+                                 uint64_t life_ticks) {
   const size_t lds = decompress_lds_bytes(kSvcMaxIn, kSvcMaxOut);
-  hipLaunchKernelGGL(lz4_decode_service_kernel, dim3(1), dim3(64), lds, st, box, gen, idle_ticks, life_ticks);
+  hipLaunchKernelGGL(lz4_decode_service_kernel, dim3(1), dim3(64), lds, st, ibox, obox, gen, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 

@@ -29,6 +29,19 @@
 //    inputs, slots past kSvcPostSlots, a post read before it was complete)
 //    the wave fetches them after an acquire fence, as before.
 //
+// Two mailboxes (round 5): an INBOX the host writes (doorbells, arguments,
+// posts, inputs, stop, active, the A/B knobs) and an OUTBOX the wave writes
+// (done words, replies, results, alive, counters).  The outbox is pinned host
+// memory: the host spins on it locally.  The inbox is fine-grained device
+// memory the host writes through the large BAR when the device has one
+// (write-combining: the host fences before each doorbell), so the wave's polls
+// and its input reads stay in its own HBM instead of crossing PCIe: a ping
+// with 112 / 2 400 / 8 192 input bytes took 2.41 / 3.03 / 4.82 us against
+// 3.71 / 6.23 / 12.31 us with the inbox in host memory, and no torn input in
+// 30 000 rounds (tools/probe/bar_probe.hip).  Without a large BAR both are the
+// same host-memory box.  Both have the SvcBox layout; each side touches only
+// its own fields of each.
+//
 // Lifetime: the host launches an instance (on a stream of its own, so two
 // instances never run at once) when it finds `alive` == 0, and stores the
 // instance's generation in `alive` first.  The wave exits after
@@ -119,7 +132,7 @@ struct SvcSlot {
 };
 
 struct SvcBox {
-  uint32_t req[kSvcSlots];         // host: a slot's request number (written last)
+  uint32_t req[kSvcSlots];         // host (inbox): a slot's request number (written last); outbox: the host's copy
   uint64_t done[kSvcSlots];        // device: (request served << 32) | return value (written last)
   SvcArgs args[kSvcSlots];         // host: the arguments of slots >= kSvcPostSlots
   uint32_t alive;                  // host: the generation it launched last (0: none); the wave clears its own
@@ -167,7 +180,7 @@ struct SvcPoll {
   uint32_t r, act, stop;
   svc_u32x4 p0, p1;
 };
-__device__ __forceinline__ SvcPoll svc_poll(SvcBox* box, uint32_t act) {
+__device__ __forceinline__ SvcPoll svc_poll(const SvcBox* box, uint32_t act) {
   const uint32_t lane = lane_id();
   SvcPoll q;
   q.r = svc_relaxed(&box->req[lane]);
@@ -178,7 +191,7 @@ __device__ __forceinline__ SvcPoll svc_poll(SvcBox* box, uint32_t act) {
   // and read as 0 without touching memory.  Cache policy 17 = sc0 | sc1
   // (system scope) on gfx950.
   const __amdgpu_buffer_rsrc_t posts = __builtin_amdgcn_make_buffer_rsrc(
-      box->post, 0, (int)(128u * (act < kSvcPostSlots ? act : kSvcPostSlots)), 0x00020000);
+      const_cast<SvcPost*>(box->post), 0, (int)(128u * (act < kSvcPostSlots ? act : kSvcPostSlots)), 0x00020000);
   q.p0 = __builtin_amdgcn_raw_buffer_load_b128(posts, (int)(16u * lane), 0, 17);
   q.p1 = __builtin_amdgcn_raw_buffer_load_b128(posts, (int)(16u * lane + 1024u), 0, 17);
   return q;
@@ -190,7 +203,7 @@ __device__ __forceinline__ SvcPoll svc_poll(SvcBox* box, uint32_t act) {
 // the slot's input go out together, one round trip; the rest, if any, all in
 // flight at once, one more.  Called after an acquire fence that follows the
 // doorbell's load, which orders these reads after the host's writes.
-__device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t* lds, uint32_t max_in) {
+__device__ __forceinline__ SvcArgs svc_fetch(const SvcBox* box, uint32_t sidx, uint8_t* lds, uint32_t max_in) {
   const uint32_t lane = lane_id();
   const bool posted = sidx < kSvcPostSlots;
   const uint32_t* ap = posted ? &box->post[sidx].csize : &box->args[sidx].csize;
@@ -228,7 +241,7 @@ __device__ __forceinline__ SvcArgs svc_fetch(SvcBox* box, uint32_t sidx, uint8_t
 // A request's input (csize bytes, known from its post) staged from the slot
 // into LDS: every chunk in flight at once, one round trip.  After an acquire
 // fence, as svc_fetch.
-__device__ __forceinline__ void svc_fetch_input(SvcBox* box, uint32_t sidx, uint8_t* lds, uint32_t csize,
+__device__ __forceinline__ void svc_fetch_input(const SvcBox* box, uint32_t sidx, uint8_t* lds, uint32_t csize,
                                                 uint32_t max_in) {
   const uint32_t lane = lane_id();
   const uint32_t n = csize < max_in ? csize : max_in;
@@ -312,33 +325,39 @@ __device__ __forceinline__ void svc_write_reply(SvcBox* box, uint32_t sidx, uint
 // The service loop shared by both kinds: polls, takes each
 // pending slot's request (from its post, or fetched), runs serve(sidx, args,
 // &res) -- the input at lds[0, csize), returning the return word after
-// writing the result bytes to box->slot[sidx].out (and setting res to the
+// writing the result bytes to obox->slot[sidx].out (and setting res to the
 // result's LDS copy, if it has one) -- then writes the reply (short results
 // in LDS) and publishes (request << 32 | rc) in the slot's done word.  Every wave reaches an exit: idle_ticks without a
 // request, life_ticks in all, or the host's stop.
 template <class Serve>
-__device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+__device__ __forceinline__ void svc_loop(const SvcBox* ibox, SvcBox* obox, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
                                          uint8_t* lds, uint32_t max_in, Serve serve) {
   const uint32_t lane = lane_id();
   // lane i: the last request of slot i served
-  uint32_t seen = (uint32_t)(__hip_atomic_load(&box->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
+  uint32_t seen = (uint32_t)(__hip_atomic_load(&obox->done[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >> 32);
   const uint64_t t0 = wall_clock64();
 #if KDB_SVC_DEBUG   // (diagnostic: instances of this box running at once)
   if (lane == 0) {
-    const uint32_t was = __hip_atomic_fetch_add(&box->pad[0], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (was != 0u) __hip_atomic_fetch_add(&box->pad[1], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t was = __hip_atomic_fetch_add(&obox->pad[0], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (was != 0u) __hip_atomic_fetch_add(&obox->pad[1], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 #endif
   uint64_t t_last = t0;
   uint32_t served = 0, polls = 0, inl = 0, rep = 0;
+#if KDB_SVC_DEBUG   // (diagnostic: wall-clock ticks spent fetching, serving, answering)
+  uint64_t dbg_fetch = 0, dbg_serve = 0, dbg_answer = 0;
+#endif
   uint32_t act = kSvcPostSlots;
-  const bool post_on = svc_relaxed(&box->no_post) == 0u, reply_on = svc_relaxed(&box->no_reply) == 0u;
+  const bool post_on = svc_relaxed(&ibox->no_post) == 0u, reply_on = svc_relaxed(&ibox->no_reply) == 0u;
   auto serve_pending = [&](uint64_t pend, const SvcPoll& q) {
 #pragma unroll 1
     while (pend) {
       const uint32_t sidx = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1u;
       const uint32_t want = readlane(q.r, sidx);
+#if KDB_SVC_DEBUG
+      const uint64_t ta = wall_clock64();
+#endif
       SvcArgs a;
       const int how = post_on ? svc_from_post(q, sidx, want, lds, &a) : 0;
       if (how == 1) {
@@ -347,17 +366,25 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
         // the doorbell's writes before the fetch's plain loads (a relaxed
         // load of the doorbell + this fence synchronise with its release)
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (how == 2) svc_fetch_input(box, sidx, lds, a.csize, max_in);   // the arguments came with the poll
-        else a = svc_fetch(box, sidx, lds, max_in);
+        if (how == 2) svc_fetch_input(ibox, sidx, lds, a.csize, max_in);   // the arguments came with the poll
+        else a = svc_fetch(ibox, sidx, lds, max_in);
       }
       const uint8_t* res = nullptr;
+#if KDB_SVC_DEBUG
+      const uint64_t tb = wall_clock64();
+#endif
       const int rc = serve(sidx, a, &res);
+#if KDB_SVC_DEBUG
+      const uint64_t tc = wall_clock64();
+      dbg_fetch += tb - ta;
+      dbg_serve += tc - tb;
+#endif
       if (res && reply_on && svc_replies(sidx, rc)) {
         // the reply carries the result; the done word only says so (kSvcReplied
         // | rc), relaxed: no wait for any earlier write to be acknowledged
-        svc_write_reply(box, sidx, want, rc, res);
+        svc_write_reply(obox, sidx, want, rc, res);
         if (lane == 0)
-          __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (kSvcReplied | (uint32_t)rc),
+          __hip_atomic_store(&obox->done[sidx], ((uint64_t)want << 32) | (kSvcReplied | (uint32_t)rc),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         rep++;
       } else {
@@ -365,10 +392,13 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
         // request and its return value, one store
         svc_release();
         if (lane == 0)
-          __hip_atomic_store(&box->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELAXED,
+          __hip_atomic_store(&obox->done[sidx], ((uint64_t)want << 32) | (uint32_t)rc, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
       }
       if (lane == sidx) seen = want;
+#if KDB_SVC_DEBUG
+      dbg_answer += wall_clock64() - tc;
+#endif
       served++;
     }
   };
@@ -394,22 +424,22 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
     // of life or at stop: these last ones, then it leaves); one that rang
     // later sees it clear and launches the next instance, which queues behind
     // this one.
-    if (lane == 0 && svc_relaxed(&box->alive) == gen) svc_store(&box->alive, 0u);
+    if (lane == 0 && svc_relaxed(&obox->alive) == gen) svc_store(&obox->alive, 0u);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    const SvcPoll q2 = svc_poll(box, act);
+    const SvcPoll q2 = svc_poll(ibox, act);
     const uint64_t pend2 = ballot(q2.r != seen);
     if (pend2 == 0) return true;
     serve_pending(pend2, q2);
     if (stop || old) return true;
-    if (lane == 0 && svc_relaxed(&box->alive) == 0u) svc_store(&box->alive, gen);
+    if (lane == 0 && svc_relaxed(&obox->alive) == 0u) svc_store(&obox->alive, gen);
     t_last = wall_clock64();
     return false;
   };
-  if (svc_relaxed(&box->no_pipe) != 0u) {
+  if (svc_relaxed(&ibox->no_pipe) != 0u) {
     // one poll in flight at a time
 #pragma unroll 1
     for (;;) {
-      const SvcPoll q = svc_poll(box, act);
+      const SvcPoll q = svc_poll(ibox, act);
       if (look(q)) break;
     }
   } else {
@@ -419,26 +449,33 @@ __device__ __forceinline__ void svc_loop(SvcBox* box, uint32_t gen, uint64_t idl
     // waits for nothing younger.  (A request answered by its done word waits,
     // at its release, for the poll in flight too.)  Unrolled by two so that
     // no poll's registers are copied while its loads are still filling them.
-    SvcPoll qa = svc_poll(box, act);
+    SvcPoll qa = svc_poll(ibox, act);
     __builtin_amdgcn_s_sleep(16);   // ~1 000 cycles: the stagger
 #pragma unroll 1
     for (;;) {
-      const SvcPoll qb = svc_poll(box, act);
+      const SvcPoll qb = svc_poll(ibox, act);
       if (look(qa)) break;
-      qa = svc_poll(box, act);
+      qa = svc_poll(ibox, act);
       if (look(qb)) break;
     }
   }
 #if KDB_SVC_DEBUG
-  if (lane == 0) __hip_atomic_fetch_sub(&box->pad[0], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) {
+    __hip_atomic_fetch_sub(&obox->pad[0], 1u, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(&obox->pad[2], (uint32_t)dbg_fetch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(&obox->pad[3], (uint32_t)dbg_serve, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(&obox->pad[4], (uint32_t)dbg_answer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(&obox->pad[5], (uint32_t)(wall_clock64() - t0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 #endif
   svc_release();
   if (lane == 0) {   // (statistics: relaxed)
-    __hip_atomic_store(&box->served, svc_relaxed(&box->served) + served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&box->polls, svc_relaxed(&box->polls) + polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&box->inline_served, svc_relaxed(&box->inline_served) + inl, __ATOMIC_RELAXED,
+    __hip_atomic_store(&obox->served, svc_relaxed(&obox->served) + served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&obox->polls, svc_relaxed(&obox->polls) + polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&obox->inline_served, svc_relaxed(&obox->inline_served) + inl, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&box->replied, svc_relaxed(&box->replied) + rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&obox->replied, svc_relaxed(&obox->replied) + rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
