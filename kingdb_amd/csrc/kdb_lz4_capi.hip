@@ -237,9 +237,9 @@ void stop_services() {
     const SvcBox* b = s->box;
     if (b->served)
       fprintf(stderr,
-              "SVCDBG kind %d wave %d: served %u polls %u launches %u; per request: fetch %.0f serve %.0f answer "
-              "%.0f ticks; wave time per poll %.1f ticks\n",
-              s->kind, s->wave, b->served, b->polls, b->launches, (double)b->pad[2] / b->served,
+              "SVCDBG kind %d wave %d: served %u (from the poll %u, replied %u) polls %u launches %u; per request: "
+              "fetch %.0f serve %.0f answer %.0f ticks; wave time per poll %.1f ticks\n",
+              s->kind, s->wave, b->served, b->inline_served, b->replied, b->polls, b->launches, (double)b->pad[2] / b->served,
               (double)b->pad[3] / b->served, (double)b->pad[4] / b->served, (double)b->pad[5] / (b->polls + 1));
 #endif
   }
