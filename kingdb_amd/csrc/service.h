@@ -263,8 +263,29 @@ __device__ __forceinline__ void svc_fetch_input(const SvcBox* box, uint32_t sidx
 // 0 when the post is not usable (then svc_fetch), 1 when the request is
 // complete, 2 when only the arguments are (its input is in the slot: then
 // svc_fetch_input).
+// The checksum's weight of dword 4 (lane & 7) + c of the post whose first lane
+// is lane & ~7 (0 for the dwords it does not cover: 0 = tag0, 30 = the sum,
+// 31 = tag1): per lane, computed once per wave.
+__device__ __forceinline__ svc_u32x4 svc_post_weights(uint32_t lane) {
+  svc_u32x4 w;
+  const uint32_t d = 4u * (lane & 7u);
+  w.x = d >= 1u ? svc_weight(d) : 0u;
+  w.y = svc_weight(d + 1u);
+  w.z = d + 2u <= 29u ? svc_weight(d + 2u) : 0u;
+  w.w = d + 3u <= 29u ? svc_weight(d + 3u) : 0u;
+  return w;
+}
+// The sum over each aligned group of 8 lanes, in every lane of the group (DPP:
+// pairs, quads, then the two quads of each half row).
+__device__ __forceinline__ uint32_t svc_sum8(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);   // row_half_mirror
+  return v;
+}
+
 __device__ __forceinline__ int svc_from_post(const SvcPoll& q, uint32_t sidx, uint32_t want, uint8_t* lds,
-                                              SvcArgs* a) {
+                                              SvcArgs* a, const svc_u32x4& pw) {
   if (sidx >= kSvcPostSlots) return 0;
   const uint32_t lane = lane_id();
   const uint32_t b = 8u * (sidx & 7u);           // the post's first lane
@@ -273,17 +294,11 @@ __device__ __forceinline__ int svc_from_post(const SvcPoll& q, uint32_t sidx, ui
                  w = hi ? q.p1.w : q.p0.w;
   const uint32_t tag0 = readlane(x, b), tag1 = readlane(w, b + 7u);
   if (tag0 != want || tag1 != want) return 0;
-  // the checksum over dwords 1-29 (dword d = 4 (lane - b) + component)
-  uint32_t part = 0;
-  if (lane >= b && lane < b + 8u) {
-    const uint32_t d0 = 4u * (lane - b);
-    part = (d0 >= 1u ? x * svc_weight(d0) : 0u) + y * svc_weight(d0 + 1u) + (d0 + 2u <= 29u ? z * svc_weight(d0 + 2u) : 0u) +
-           (d0 + 3u <= 29u ? w * svc_weight(d0 + 3u) : 0u);
-  }
-  uint32_t sum = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < 8u; ++j) sum += readlane(part, b + j);
-  if (sum != readlane(z, b + 7u)) return 0;
+  // the checksum over dwords 1-29 (dword d = 4 (lane - b) + component): each
+  // lane's share, summed over the post's 8 lanes (the other groups sum other
+  // posts, unused here)
+  const uint32_t sum = svc_sum8(x * pw.x + y * pw.y + z * pw.z + w * pw.w);
+  if (readlane(sum, b) != readlane(z, b + 7u)) return 0;
   a->csize = readlane(y, b);
   a->osize = readlane(z, b);
   a->target = readlane(w, b);
@@ -306,15 +321,12 @@ __device__ __forceinline__ void svc_write_reply(SvcBox* box, uint32_t sidx, uint
     const uint4 x = reinterpret_cast<const uint4*>(res)[lane - 1u];
     d = svc_u32x4{x.x, x.y, x.z, x.w};
   }
-  uint32_t part = 0;
-  if (lane >= 1u && lane < 8u) {
-    const uint32_t i0 = 4u * (lane - 1u);
-    part = d.x * svc_weight(i0) + d.y * svc_weight(i0 + 1u) + d.z * svc_weight(i0 + 2u);
-    if (lane < 7u) part += d.w * svc_weight(i0 + 3u);   // lane 7's last dword is tag1
-  }
-  uint32_t sum = 0;
-#pragma unroll
-  for (uint32_t j = 1; j < 8u; ++j) sum += readlane(part, j);
+  // the checksum: lane j's share (data dwords 4 (j - 1) .. + 3; lane 7's last
+  // dword is tag1), summed over lanes 0-7 (svc_sum8; lane 0's data is 0)
+  const uint32_t i0 = 4u * (lane - 1u);
+  const uint32_t part = d.x * svc_weight(i0) + d.y * svc_weight(i0 + 1u) + d.z * svc_weight(i0 + 2u) +
+                        (lane < 7u ? d.w * svc_weight(i0 + 3u) : 0u);
+  const uint32_t sum = readlane(svc_sum8(part), 0);
   if (lane == 0u) d = svc_u32x4{want, (uint32_t)rc, sum, 0u};
   if (lane == 7u) d.w = want;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(&box->reply[sidx], 0, 128, 0x00020000);
@@ -349,6 +361,7 @@ __device__ __forceinline__ void svc_loop(const SvcBox* ibox, SvcBox* obox, uint3
 #endif
   uint32_t act = kSvcPostSlots;
   const bool post_on = svc_relaxed(&ibox->no_post) == 0u, reply_on = svc_relaxed(&ibox->no_reply) == 0u;
+  const svc_u32x4 pw = svc_post_weights(lane);
   auto serve_pending = [&](uint64_t pend, const SvcPoll& q) {
 #pragma unroll 1
     while (pend) {
@@ -359,7 +372,7 @@ __device__ __forceinline__ void svc_loop(const SvcBox* ibox, SvcBox* obox, uint3
       const uint64_t ta = wall_clock64();
 #endif
       SvcArgs a;
-      const int how = post_on ? svc_from_post(q, sidx, want, lds, &a) : 0;
+      const int how = post_on ? svc_from_post(q, sidx, want, lds, &a, pw) : 0;
       if (how == 1) {
         inl++;
       } else {
