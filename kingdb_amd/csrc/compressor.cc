@@ -48,9 +48,30 @@ const Crc32cTables& crc_tables() {
 }
 }  // namespace
 
+#if defined(__x86_64__)
+// The same CRC with SSE4.2's crc32 instruction (the Castagnoli polynomial):
+// every Uncompress streams its frame through the CRC (compressor.cc:126), so a
+// 4 KiB Get pays ~2.4 KB of it on the host.
+static __attribute__((target("sse4.2"))) uint32_t crc32c_extend_hw(uint32_t crc, const uint8_t* p, size_t n) {
+  uint64_t l = crc ^ 0xffffffffu;
+  for (; n >= 8; n -= 8, p += 8) {
+    uint64_t w;
+    memcpy(&w, p, 8);
+    l = __builtin_ia32_crc32di(l, w);
+  }
+  uint32_t c = (uint32_t)l;
+  for (; n; n--) c = __builtin_ia32_crc32qi(c, *p++);
+  return c ^ 0xffffffffu;
+}
+static const bool kHwCrc32c = __builtin_cpu_supports("sse4.2");
+#endif
+
 uint32_t Crc32cExtend(uint32_t crc, const char* data, size_t n) {
-  const Crc32cTables& T = crc_tables();
   const uint8_t* p = reinterpret_cast<const uint8_t*>(data);
+#if defined(__x86_64__)
+  if (kHwCrc32c) return crc32c_extend_hw(crc, p, n);
+#endif
+  const Crc32cTables& T = crc_tables();
   uint32_t l = crc ^ 0xffffffffu;
   while (n >= 8) {
     uint32_t lo = l ^ ((uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24);

@@ -990,7 +990,11 @@ __global__ __launch_bounds__(64) void lz4_decode_service_kernel(const SvcBox* ib
     if (csize >= 0 && osize >= 0 && (uint32_t)csize <= kSvcMaxIn && (uint32_t)osize <= kSvcMaxOut) {
       if (lane < 16u) s_in[(uint32_t)csize + lane] = 0;   // OOB bytes read as 0
       __syncthreads();
+#if KDB_ABL_SVC_NOSERVE   // (attribution build: no decode, the output claimed -- timing only)
+      rc = osize;
+#else
       rc = decode_block(s_in, 0u, csize, s_out, osize, tgt);
+#endif
       // a short result goes back in the slot's reply (svc_loop), the rest here
       if (rc > 0 && !(reply_on && svc_replies(sidx, rc))) flush_lds_to_global(obox->slot[sidx].out, s_out, 0, (uint32_t)rc);
       *res = s_out;   // the reply reads it before the next request's staging

@@ -55,6 +55,9 @@ static double now_us() {
 int main(int argc, char** argv) {
   const uint64_t size = argc > 1 ? strtoull(argv[1], nullptr, 0) : 100;
   const int calls = argc > 2 ? atoi(argv[2]) : 2000;
+  // KDB_BENCH_NOVERIFY=1: timing-only library builds (attribution variants
+  // whose output is wrong by design) skip the byte check
+  const bool verify = !getenv("KDB_BENCH_NOVERIFY");
   const std::string pool = g1_pool(size * (uint64_t)calls + 1);
   kdb::CompressorLZ4 lz4;
   std::vector<char*> frames(calls, nullptr);
@@ -78,7 +81,7 @@ int main(int argc, char** argv) {
       char *out = nullptr, *frame = nullptr;
       uint64_t n = 0, fn = 0;
       kdb::Status s = lz4.Uncompress(frames[i], flen[i], &out, &n, &frame, &fn);
-      if (!s.IsOK() || n != size || memcmp(out, pool.data() + size * i, size) != 0) {
+      if (!s.IsOK() || (verify && (n != size || memcmp(out, pool.data() + size * i, size) != 0))) {
         fprintf(stderr, "Uncompress failed or differs at %d\n", i);
         return 1;
       }
