@@ -123,6 +123,7 @@ static_assert(kT12Lo == 4096u && kT12Hi == kT12Lo + 8192u, "value, then the 8 Ki
 #define KDB_STR2(x) #x
 #define KDB_STR(x) KDB_STR2(x)
 struct Table12 {
+  static constexpr bool kTagged = false;
   // a lane's slot as the exchange addressed it, kept for restore(): the low
   // byte's index, the high nibble's dword address (in its plane) and shift
   struct Slot { uint32_t lo, hi, sh, mh; };
@@ -181,6 +182,7 @@ constexpr uint32_t kOffLaneLds = 0x10000u;
 
 // byU16 table, 8192 x u16 (values up to 65 546 bytes; positions < 65 536).
 struct Table16 {
+  static constexpr bool kTagged = false;
   uint32_t off;
   struct Slot { uint32_t h; };
   __device__ Table16(uint16_t* p) : off(lds_off(p)) {}
@@ -201,6 +203,7 @@ struct Table16 {
 
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
 struct Table32 {
+  static constexpr bool kTagged = false;
   uint32_t off;
   struct Slot { uint32_t h; };
   __device__ Table32(uint32_t* p) : off(lds_off(p)) {}
@@ -210,6 +213,39 @@ struct Table32 {
     return mskor_rtn(off + (s.h << 2), 0xffffffffu, p);
   }
   __device__ __forceinline__ void restore(const Slot& s, uint32_t v) const { ((lds_u32*)(uintptr_t)off)[s.h] = v; }
+};
+
+// byU32 table with word tags (values of at most kTagMaxLen bytes: positions fit
+// 20 bits).  An entry is position | tag << 20, the tag 12 more bits of the
+// entry's 4-byte word (bits 8-19 of the hash product; the hash takes bits
+// 20-31).  Two words with different tags differ, so a candidate whose tag is
+// not the searched word's -- or whose position is past the 64 KiB window --
+// cannot match (lz4.cc:526-527), and its 4 bytes are not read: the reads left
+// are mostly true matches near the search, hits in this wave's cache lines,
+// instead of stale entries scattered over the value's past (L2/MALL misses on
+// 1 MiB parts).  The same decisions and the same table contents, positions-
+// wise, as Table32.  An empty entry is position 0 with position 0's tag
+// (empty()): the reference's empty slots read as position 0, whose word may
+// match.
+constexpr uint32_t kTagMaxLen = 1u << 20;
+__device__ __forceinline__ uint32_t word_tag(uint32_t seq) { return ((seq * 2654435761u) >> 8) & 0xfffu; }
+struct Table32T {
+  static constexpr bool kTagged = true;
+  uint32_t off;
+  struct Slot { uint32_t h, e; };
+  __device__ Table32T(uint32_t* p) : off(lds_off(p)) {}
+  __device__ Table32T() : off(0) {}
+  __device__ __forceinline__ static uint32_t empty(uint32_t word0) { return word_tag(word0) << 20; }
+  // get + put with the tag; *maybe: the old entry's tag is tg (the lane is on)
+  __device__ __forceinline__ uint32_t xchg_tagged(uint32_t h, uint32_t p, uint32_t tg, bool on, Slot& s,
+                                                  bool& maybe) const {
+    s.h = h | (on ? 0u : 0x4000u);      // an off lane: past the allocation (see Table12::xchg)
+    s.e = mskor_rtn(off + (s.h << 2), 0xffffffffu, p | (tg << 20));
+    maybe = on && (s.e >> 20) == tg;
+    return s.e & 0xfffffu;
+  }
+  // the entry as this lane read it (v, its position, is implied)
+  __device__ __forceinline__ void restore(const Slot& s, uint32_t) const { ((lds_u32*)(uintptr_t)off)[s.h] = s.e; }
 };
 
 // Value bytes staged in LDS (byte i at p[i]).  kUnclamped: a read outside the
@@ -801,7 +837,13 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         const uint32_t h = hashp<kWide>(seq);
         // get + put of every valid lane at once, in lane order: refk is the
         // entry as the sequential loop's get at this iteration reads it
-        refk = tab.xchg(h, pk, valid, slot);
+        bool maybe = true;
+        if constexpr (Tab::kTagged) {
+          refk = tab.xchg_tagged(h, pk, word_tag(seq), valid, slot, maybe);
+          maybe = maybe && pk <= refk + kMaxDistance;
+        } else {
+          refk = tab.xchg(h, pk, valid, slot);
+        }
 #if KDB_ABL_DUP_CAND
         {  // attribution build: the candidate word read twice (opaque address, so both loads stay)
           uint32_t r2 = refk;
@@ -816,7 +858,14 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // distance check (lz4.cc:526, 614), byU16 sizes never need it.
         // refk is a position <= mflimit of this value (the table holds
         // nothing else), so its 4 bytes need no clamp.
-        mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) &
+        uint32_t cw;
+        if constexpr (Tab::kTagged) {   // only candidates that may match are read
+          cw = ~seq;
+          if (maybe) cw = RD32(refk);
+        } else {
+          cw = RD32(refk);
+        }
+        mm = __builtin_amdgcn_uicmp(cw, seq, 32 /*EQ*/) &
              (t0 ? __builtin_amdgcn_sicmp(key_match, bound, 41 /*SLE*/) : vm);
         if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
       }
@@ -836,8 +885,17 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           const bool valid = __builtin_amdgcn_inverse_ballot_w64(vm);
           const uint32_t seq = RD32(clamp4(pk));
           const uint32_t h = hashp<kWide>(seq);
-          refk = tab.xchg(h, pk, valid, slot);
-          mm = __builtin_amdgcn_uicmp(RD32(refk), seq, 32 /*EQ*/) & vm;
+          uint32_t cw;
+          if constexpr (Tab::kTagged) {
+            bool maybe;
+            refk = tab.xchg_tagged(h, pk, word_tag(seq), valid, slot, maybe);
+            cw = ~seq;
+            if (maybe && pk <= refk + kMaxDistance) cw = RD32(refk);
+          } else {
+            refk = tab.xchg(h, pk, valid, slot);
+            cw = RD32(refk);
+          }
+          mm = __builtin_amdgcn_uicmp(cw, seq, 32 /*EQ*/) & vm;
           if (kWide) mm &= __builtin_amdgcn_uicmp(pk, refk + kMaxDistance, 37 /*ULE*/);
           if ((mm | ~vm) != 0) break;                // a match, or past mflimit
         }
@@ -1141,6 +1199,7 @@ __device__ __forceinline__ void big_values(
   Tab tab;
   if constexpr (kWide) tab = Table32(tab32);
   else tab = Table16(reinterpret_cast<uint16_t*>(tab32));
+  const Table32T tabt(tab32);
   bool direct_done = false;
 #pragma unroll 1
   for (;;) {
@@ -1166,19 +1225,31 @@ __device__ __forceinline__ void big_values(
       const uint32_t S = readlane(len, l);
       const uint8_t* g = src + src_off[v];
       uint8_t* o = dst + dst_off[v];
-      for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(0, 0, 0, 0);
+      // byU32 values of at most kTagMaxLen bytes (KingDB's 1 MB parts) take the
+      // tagged table, whose empty entries hold position 0's tag
+      const bool tagged = kWide && S <= kTagMaxLen && S >= 4u;
+      const uint32_t fill = tagged ? Table32T::empty(uni(*reinterpret_cast<const GlobalSrc::u32u*>(g))) : 0u;
+      for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(fill, fill, fill, fill);
       const uint32_t bound = compress_bound(S);                   // 0 past LZ4_MAX_INPUT_SIZE
       GlobalSrc ws{g, S, 0u};
+      // compress_block over the value with table T (cap: the caller's; out: o + skip)
+      auto run = [&](const auto& t, uint32_t skip, int cap, int b) -> int {
+        return cap < b ? compress_block<kWide, true>(ws, S, t, o + skip, cap, cap)
+                       : compress_block<kWide, false>(ws, S, t, o + skip, b, cap);
+      };
+      auto run_any = [&](uint32_t skip, int cap, int b) -> int {
+        if constexpr (kWide) {
+          if (tagged) return run(tabt, skip, cap, b);
+        }
+        return run(tab, skip, cap, b);
+      };
       if (!kFrame) {
         const uint32_t cap = uni(dst_cap[v]);
         int r = 0;
-        if (bound != 0)
-          r = cap < bound ? compress_block<kWide, true>(ws, S, tab, o, (int)cap, (int)cap)
-                          : compress_block<kWide, false>(ws, S, tab, o, (int)bound, (int)cap);
+        if (bound != 0) r = run_any(0u, (int)cap, (int)bound);
         if (lane == 0) ret[v] = r;
       } else {
-        const int r =
-            bound == 0 ? 0 : compress_block<kWide, false>(ws, S, tab, o + 8, (int)bound, (int)bound);
+        const int r = bound == 0 ? 0 : run_any(8u, (int)bound, (int)bound);
         if (r <= 0) {                                             // compressor.cc:31-34
           if (lane == 0) { ret[v] = -1; frame_len[v] = 0; }
         } else {

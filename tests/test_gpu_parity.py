@@ -330,6 +330,35 @@ def test_big_values_byu32(gpu, orc):
     assert all(st == 0 and out == x for (st, out), x in zip(mb, mixed))
 
 
+def test_byu32_tagged_table_edges(gpu, orc):
+    """The tagged byU32 table (lz4_compress.hip Table32T, values <= 1 MiB): its empty
+    entries stand for position 0, whose word may match later (a value whose only
+    repeats are of its first 4 bytes); values just under and over the 1 MiB tag limit,
+    matches just inside and outside the 64 KiB window, and a value repeated whole from
+    past the window.  Frames equal the oracle's."""
+    rng = np.random.default_rng(2024)
+    vals = []
+    for n in (65547, 100000, (1 << 20) - 1, 1 << 20, (1 << 20) + 1, (1 << 20) + 70000):
+        x = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        w0 = bytes(x[:4])
+        for at in rng.integers(5, n - 8, 40):   # position 0's word, scattered
+            x[int(at):int(at) + 4] = w0
+        vals.append(bytes(x))
+    # a repeat just inside / just outside the window (65 535 / 65 536 back)
+    base = bytearray(rng.integers(0, 256, 200000, dtype=np.uint8).tobytes())
+    for d in (65535, 65536, 65537):
+        y = bytearray(base)
+        y[150000:150032] = y[150000 - d:150000 - d + 32]
+        vals.append(bytes(y))
+    # a value repeated whole, 150 000 bytes back (past the window)
+    z = bytearray(rng.integers(0, 256, 300000, dtype=np.uint8).tobytes())
+    vals.append(bytes(z[:150000]) * 2)
+    frames = gpu.compress_frames(vals)
+    assert frames == [orc.frame(v) for v in vals]
+    back = gpu.decompress_frames(frames, [len(v) for v in vals])
+    assert all(st == 0 and out == v for (st, out), v in zip(back, vals))
+
+
 def test_big_scalar_mirrors(gpu, orc):
     pool = oracle.g1_pool(orc).tobytes()
     x = pool[:300000]
