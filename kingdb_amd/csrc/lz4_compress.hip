@@ -374,6 +374,15 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
   return x;
 }
 
+// The per-sequence register window (compress_block's kWin) for tagged byU32
+// values too: with the table's tags most candidate reads are near matches, so
+// the window's bytes serve the count, the literals and the next input words
+// (1 MiB parts: compress 22.3-22.7 -> 20.0 ms; untagged, it measured slower,
+// profiles/r04_d/r04_y2_ab_window_byu32.txt).
+#ifndef KDB_LZ4_WIDE_WINDOW
+#define KDB_LZ4_WIDE_WINDOW 1
+#endif
+
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
 // or 0 (limitedOutput failure, checked against `cap` at the reference's check
@@ -421,7 +430,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // A base of 2^31 marks "no window" (positions stay below 2^31).  byU16
     // values only: for byU32 ones (1 MiB parts) it measured slower (8.47 ->
     // 9.01 ms per 600 x 1 MiB).
-    constexpr bool kWin = !kFree && !kWide;
+    constexpr bool kWin = !kFree && (!kWide || (KDB_LZ4_WIDE_WINDOW && Tab::kTagged));
 #ifndef KDB_LZ4_SEQ_WINDOW
 #define KDB_LZ4_SEQ_WINDOW 1
 #endif

@@ -15,7 +15,8 @@
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the headline -> pmc_traffic.json
 #   pmcmixed   the same for the mixed batch
 #   pmcu:<size>:<values>  the same for a uniform batch of other sizes
-#   sq         SQ counter passes of the headline (tools/pmc.sh)
+#   sq         SQ counter passes of the headline (tools/pmc.sh); sqbig: of the big workload
+#   profbig    rocprofv3 --kernel-trace --stats of the big workload
 #   dropin     KingDB's unit tests built against the drop-in (tests/test_kingdb_dropin.py)
 #   dropinfull the same with the whole test_db and client_emb (KDB_DROPIN_FULL=1)
 #   hook       the flush-hook build's tests only (test_kingdb_dropin.py -k hook)
@@ -73,6 +74,7 @@ for s in "$@"; do
     profmixed) prof mixed --workload mixed --no-cpu-baseline --steps 3 --warmup 1 ;;
     profput) prof put --workload put --no-cpu-baseline --steps 3 --warmup 1 ;;
     profget) prof get --workload get --no-cpu-baseline --steps 3 --warmup 1 ;;
+    profbig) prof big --workload big --no-cpu-baseline --steps 3 --warmup 1 ;;
     pmc) pmc bench 1048576 4096 ;;
     pmcmixed) pmc mixed 1048576 mixed --workload mixed ;;
     pmcu:*)   # pmcu:<size>:<values> -- FETCH/WRITE passes of a uniform batch
@@ -81,6 +83,9 @@ for s in "$@"; do
     sq)
       timeout -k 10 900 bash tools/pmc.sh "${O}_sq" python3 "$R/bench.py" --no-cpu-baseline --no-host-inclusive --no-verify --steps 1 --warmup 0 || exit 1
       python tools/pmc_summary.py "${O}_sq" > "${O}_sq.txt" && cat "${O}_sq.txt" ;;
+    sqbig)
+      timeout -k 10 900 bash tools/pmc.sh "${O}_sqbig" python3 "$R/bench.py" --workload big --no-cpu-baseline --no-verify --steps 1 --warmup 0 || exit 1
+      python tools/pmc_summary.py "${O}_sqbig" > "${O}_sqbig.txt" && cat "${O}_sqbig.txt" ;;
     dropin|dropinfull)
       [ $s = dropinfull ] && export KDB_DROPIN_FULL=1
       timeout -k 10 1100 python -u -m pytest tests/test_kingdb_dropin.py -x -v -s -m gpu --durations=0 --timeout 1000 --timeout-method thread > "${O}_$s.log" 2>&1 || fail $s $? "${O}_$s.log"
