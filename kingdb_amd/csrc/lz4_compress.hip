@@ -248,11 +248,40 @@ struct Table32T {
   __device__ __forceinline__ void restore(const Slot& s, uint32_t) const { ((lds_u32*)(uintptr_t)off)[s.h] = s.e; }
 };
 
+// The per-sequence register window (compress_block's kWin) for tagged byU32
+// values too: with the table's tags most candidate reads are near matches, so
+// the window's bytes serve the count, the literals and the next input words
+// (1 MiB parts: compress 22.3-22.7 -> 20.0 ms; untagged, it measured slower,
+// profiles/r04_d/r04_y2_ab_window_byu32.txt).
+#ifndef KDB_LZ4_WIDE_WINDOW
+#define KDB_LZ4_WIDE_WINDOW 1
+#endif
+// byU32 values with the tagged table read through an LDS ring (RingSrc)
+// instead of in place with the register window: 1 MiB parts compress
+// 20.0 -> 15.3 ms (profiles/r05/r05_rg*: a 4 KiB ring refilled 1 KiB at a
+// time when the search comes within 512 bytes of its front; a 2 KiB ring
+// measured the same, 8 KiB or a 2 KiB front slower, and loading the next
+// chunk a refill ahead slower too -- its loads, in flight, then sat in front
+// of every other global access's in-order wait).
+#ifndef KDB_LZ4_WIDE_RING
+#define KDB_LZ4_WIDE_RING 1
+#endif
+#ifndef KDB_LZ4_RING_AHEAD
+#define KDB_LZ4_RING_AHEAD 0
+#endif
+#ifndef KDB_LZ4_RING_BYTES
+#define KDB_LZ4_RING_BYTES 4096u
+#endif
+#ifndef KDB_LZ4_RING_FRONT
+#define KDB_LZ4_RING_FRONT 512u
+#endif
+
 // Value bytes staged in LDS (byte i at p[i]).  kUnclamped: a read outside the
 // value cannot fault (LDS), so the parse's reads whose result a lane mask
 // discards need no clamp into [0, S).
 struct LdsSrc {
   static constexpr bool kUnclamped = true;
+  static constexpr bool kWindow = false;
   const uint8_t* p;
   __device__ __forceinline__ uint32_t u8(uint32_t i) const { return p[i]; }
   __device__ __forceinline__ uint32_t rd32(uint32_t i) const { return lds_rd32(p, i); }
@@ -269,6 +298,7 @@ struct LdsSrc {
 // Value bytes read in place from global memory (any alignment).
 struct GlobalSrc {
   static constexpr bool kUnclamped = false;
+  static constexpr bool kWindow = true;    // compress_block's per-sequence register window
   const uint8_t* g;
   uint32_t S;
   uint32_t keep;   // the frontier touch in flight (see step)
@@ -289,6 +319,93 @@ struct GlobalSrc {
     asm volatile("" ::"v"(keep));
     const uint32_t a = min(p + 256u + 4u * lane_id(), S - 1u);
     keep = *reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(g + a) & ~(uintptr_t)3);
+  }
+};
+
+__device__ __forceinline__ uint4 funnel16(const uint4& a, const uint4& b, uint32_t sh);
+// Value bytes of a long value read through an LDS ring of its last kR bytes
+// (byU32 values with the tagged table): every read the parse makes near the
+// search -- the input words, the count's bytes, the literals, the near
+// candidates the tags leave -- is an LDS read; positions outside the ring
+// (far candidates, a long count past the front) fall back to global loads.
+// Global loads return in issue order (vmcnt), so with the value read in place
+// each sequence waited for its own frontier's HBM miss (the frontier touch
+// only moved the wait); here the value comes in 1 KiB refills, one wait per
+// ~10 G1 sequences.  The ring holds positions [hi - kR, hi) at ring + (p mod
+// kR), with a kMirror-byte copy of its first bytes after its end so a 4-byte
+// read never wraps.
+struct RingSrc {
+  static constexpr bool kUnclamped = false;   // compress_block clamps (the fallback reads global memory)
+  static constexpr bool kWindow = false;
+  static constexpr uint32_t kR = KDB_LZ4_RING_BYTES, kMirror = 64u, kChunk = 1024u, kFront = KDB_LZ4_RING_FRONT;
+  typedef uint32_t __attribute__((aligned(1))) u32u;
+  const uint8_t* g;
+  uint32_t S;
+  uint8_t* ring;        // LDS: kR + kMirror bytes, 16-byte aligned
+  uint32_t hi;          // positions below hi are staged (the last kR of them are in the ring)
+  __device__ __forceinline__ bool in(uint32_t i, uint32_t n) const { return i - (hi - kR) <= kR - n; }
+  __device__ __forceinline__ uint32_t u8(uint32_t i) const {
+    uint32_t v = ring[i & (kR - 1u)];
+    const bool ok = in(i, 1u);
+    if (ballot(!ok)) {
+      if (!ok) v = g[i];
+    }
+    return v;
+  }
+  __device__ __forceinline__ uint32_t rd32(uint32_t i) const {
+    uint32_t v = lds_rd32(ring, i & (kR - 1u));
+    const bool ok = in(i, 4u);
+    if (ballot(!ok)) {
+      if (!ok) v = *reinterpret_cast<const u32u*>(g + i);
+    }
+    return v;
+  }
+  struct Word { uint32_t v; };
+  __device__ __forceinline__ Word rd32_issue(uint32_t i) const { return Word{rd32(i)}; }
+  __device__ __forceinline__ static uint32_t word(const Word& w) { return w.v; }
+  // Before a sequence's search from p: the ring filled to kFront past p (or
+  // the value's end), 1 KiB at a time -- whole aligned 16-byte loads (an
+  // aligned chunk never crosses a page, so reading around the value cannot
+  // fault), realigned in registers.  With KDB_LZ4_RING_AHEAD the next chunk's
+  // loads go out at the end of each refill and land in registers (na, nb)
+  // until the front needs them, so a refill rarely waits.
+  uint4 na, nb;
+  bool npend;
+  __device__ __forceinline__ void fetch(uint32_t at, uint4& a, uint4& b) const {
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+    const uint4* base = reinterpret_cast<const uint4*>(g - head);
+    const uint32_t c = (at >> 4) + lane_id();   // this lane's 16 bytes: positions at + 16 lane ..
+    a = base[c];
+    b = head ? base[c + 1u] : a;
+  }
+  __device__ __forceinline__ void put(const uint4& a, const uint4& b) {
+    const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
+    const uint4 w = funnel16(a, b, head);
+    const uint32_t o = (hi & (kR - 1u)) + 16u * lane_id();
+    reinterpret_cast<uint4*>(ring)[o >> 4] = w;
+    if (o < kMirror) reinterpret_cast<uint4*>(ring)[(kR + o) >> 4] = w;
+    hi += kChunk;
+  }
+  __device__ __forceinline__ void step(uint32_t p) {
+#pragma unroll 1
+    while (hi < S && p + kFront > hi) {
+#if KDB_LZ4_RING_AHEAD
+      if (npend) {
+        put(na, nb);
+        npend = false;
+        continue;
+      }
+#endif
+      uint4 a, b;
+      fetch(hi, a, b);
+      put(a, b);
+    }
+#if KDB_LZ4_RING_AHEAD
+    if (!npend && hi < S) {
+      fetch(hi, na, nb);
+      npend = true;
+    }
+#endif
   }
 };
 
@@ -374,14 +491,6 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
   return x;
 }
 
-// The per-sequence register window (compress_block's kWin) for tagged byU32
-// values too: with the table's tags most candidate reads are near matches, so
-// the window's bytes serve the count, the literals and the next input words
-// (1 MiB parts: compress 22.3-22.7 -> 20.0 ms; untagged, it measured slower,
-// profiles/r04_d/r04_y2_ab_window_byu32.txt).
-#ifndef KDB_LZ4_WIDE_WINDOW
-#define KDB_LZ4_WIDE_WINDOW 1
-#endif
 
 // LZ4_compress_generic (byU16, limitedOutput).  `in` = LDS, value byte i at
 // in[i], i < S (every read is clamped into [0, S)).  Returns the block size
@@ -430,7 +539,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
     // A base of 2^31 marks "no window" (positions stay below 2^31).  byU16
     // values only: for byU32 ones (1 MiB parts) it measured slower (8.47 ->
     // 9.01 ms per 600 x 1 MiB).
-    constexpr bool kWin = !kFree && (!kWide || (KDB_LZ4_WIDE_WINDOW && Tab::kTagged));
+    constexpr bool kWin = !kFree && Src::kWindow && (!kWide || (KDB_LZ4_WIDE_WINDOW && Tab::kTagged));
 #ifndef KDB_LZ4_SEQ_WINDOW
 #define KDB_LZ4_SEQ_WINDOW 1
 #endif
@@ -1198,7 +1307,7 @@ size_t compress_lds_bytes(uint32_t max_len) {
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
 template <bool kFrame, bool kWide>
 __device__ __forceinline__ void big_values(
-    uint32_t* const tab32, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    uint32_t* const tab32, uint8_t* const ring, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
@@ -1241,16 +1350,24 @@ __device__ __forceinline__ void big_values(
       for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(fill, fill, fill, fill);
       const uint32_t bound = compress_bound(S);                   // 0 past LZ4_MAX_INPUT_SIZE
       GlobalSrc ws{g, S, 0u};
-      // compress_block over the value with table T (cap: the caller's; out: o + skip)
-      auto run = [&](const auto& t, uint32_t skip, int cap, int b) -> int {
-        return cap < b ? compress_block<kWide, true>(ws, S, t, o + skip, cap, cap)
-                       : compress_block<kWide, false>(ws, S, t, o + skip, b, cap);
+      // compress_block over the value with source R and table T (cap: the
+      // caller's; out: o + skip)
+      auto run = [&](auto& rsrc, const auto& t, uint32_t skip, int cap, int b) -> int {
+        return cap < b ? compress_block<kWide, true>(rsrc, S, t, o + skip, cap, cap)
+                       : compress_block<kWide, false>(rsrc, S, t, o + skip, b, cap);
       };
       auto run_any = [&](uint32_t skip, int cap, int b) -> int {
         if constexpr (kWide) {
-          if (tagged) return run(tabt, skip, cap, b);
+          if (tagged) {
+#if KDB_LZ4_WIDE_RING
+            RingSrc rs{g, S, ring, 0u, {}, {}, false};
+            return run(rs, tabt, skip, cap, b);
+#else
+            return run(ws, tabt, skip, cap, b);
+#endif
+          }
         }
-        return run(tab, skip, cap, b);
+        return run(ws, tab, skip, cap, b);
       };
       if (!kFrame) {
         const uint32_t cap = uni(dst_cap[v]);
@@ -1298,7 +1415,9 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   // arbitration over the small classes' waves that fill the GPU beside them
   if (prio) __builtin_amdgcn_s_setprio(2);
   __shared__ __attribute__((aligned(16))) uint32_t tab32[4096];
-  big_values<kFrame, kWide>(tab32, src, src_off, src_len, n, min_len, max_len, dst, dst_off, dst_cap, frame_len,
+  // byU32 values' LDS ring (RingSrc); 16 + 4.06 KiB: 7 waves per CU (LDS)
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kWide && KDB_LZ4_WIDE_RING ? RingSrc::kR + RingSrc::kMirror : 16u];
+  big_values<kFrame, kWide>(tab32, ring, src, src_off, src_len, n, min_len, max_len, dst, dst_off, dst_cap, frame_len,
                             ret, work, batch);
 }
 
@@ -1319,7 +1438,7 @@ __global__ __launch_bounds__(64) void lz4_compress_mixed_kernel(
     uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work_big,
     uint32_t batch_big, uint32_t* __restrict__ work_small, uint32_t batch_small, uint32_t nq) {
   __shared__ __attribute__((aligned(16))) uint32_t smem32[(kTable12Bytes + kSmallMax) / 4u];
-  big_values<kFrame, false>(smem32, src, src_off, src_len, n, big_min, big_max, dst, dst_off, dst_cap, frame_len,
+  big_values<kFrame, false>(smem32, nullptr, src, src_off, src_len, n, big_min, big_max, dst, dst_off, dst_cap, frame_len,
                             ret, work_big, batch_big);
   __syncthreads();
 #ifndef KDB_LZ4_MIXED_EMIT
