@@ -69,7 +69,8 @@ def parse():
     p.add_argument("--put-chunk", type=int, default=1 << 17, help="put workload: puts per pipeline chunk")
     p.add_argument("--pmc", default=None,
                    help="HBM traffic summary written by tools/pmc_traffic.py (default: "
-                        "profiles/pmc_traffic.json, profiles/pmc_traffic_mixed.json for --workload mixed)")
+                        "profiles/pmc_traffic.json, profiles/pmc_traffic_mixed.json for --workload mixed, "
+                        "profiles/pmc_traffic_big.json for --workload big)")
     a = p.parse_args()
     if a.values is None:
         a.values = 2560 if a.workload == "big" else 1 << 20
@@ -653,8 +654,9 @@ def main() -> None:
     # workload (tools/pmc_traffic.py); used only when the passes were taken with
     # this very build (kdb_lz4_build_id) and name the kernels this run queued
     traffic, traffic_source, traffic_refused = None, None, None
-    pmc = args.pmc or os.path.join(ROOT, "profiles",
-                                   "pmc_traffic_mixed.json" if args.workload == "mixed" else "pmc_traffic.json")
+    pmc = args.pmc or os.path.join(ROOT, "profiles", {"mixed": "pmc_traffic_mixed.json",
+                                                      "big": "pmc_traffic_big.json"}.get(args.workload,
+                                                                                         "pmc_traffic.json"))
     try:
         pm = json.load(open(pmc))
         want = (args.values, "mixed") if args.workload == "mixed" else (n, size)

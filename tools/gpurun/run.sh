@@ -13,7 +13,7 @@
 #   prof       rocprofv3 --kernel-trace --stats of the headline bench
 #   profmixed profput profget   the same for the other workloads
 #   pmc        FETCH_SIZE / WRITE_SIZE passes of the headline -> pmc_traffic.json
-#   pmcmixed   the same for the mixed batch
+#   pmcmixed   the same for the mixed batch; pmcbig: for the 1 MiB parts
 #   pmcu:<size>:<values>  the same for a uniform batch of other sizes
 #   sq         SQ counter passes of the headline (tools/pmc.sh); sqbig: of the big workload
 #   profbig    rocprofv3 --kernel-trace --stats of the big workload
@@ -77,6 +77,7 @@ for s in "$@"; do
     profbig) prof big --workload big --no-cpu-baseline --steps 3 --warmup 1 ;;
     pmc) pmc bench 1048576 4096 ;;
     pmcmixed) pmc mixed 1048576 mixed --workload mixed ;;
+    pmcbig) pmc big 2560 1048576 --workload big ;;
     pmcu:*)   # pmcu:<size>:<values> -- FETCH/WRITE passes of a uniform batch
       a=${s#pmcu:}; sz=${a%%:*}; nv=${a#*:}
       pmc u${sz} $nv $sz --size $sz --values $nv ;;
