@@ -371,12 +371,17 @@ struct RingSrc {
   // until the front needs them, so a refill rarely waits.
   uint4 na, nb;
   bool npend;
+  // Only aligned chunks that hold a byte of the value are loaded (a chunk past
+  // its end may lie past the allocation: zeros instead); the ring's bytes past
+  // S are never used (compress_block clamps its reads into the value).
   __device__ __forceinline__ void fetch(uint32_t at, uint4& a, uint4& b) const {
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
     const uint4* base = reinterpret_cast<const uint4*>(g - head);
     const uint32_t c = (at >> 4) + lane_id();   // this lane's 16 bytes: positions at + 16 lane ..
-    a = base[c];
-    b = head ? base[c + 1u] : a;
+    const uint32_t end = head + S;               // chunk k holds value bytes iff 16 k < end
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    a = 16u * c < end ? base[c] : z;
+    b = head ? (16u * (c + 1u) < end ? base[c + 1u] : z) : a;
   }
   __device__ __forceinline__ void put(const uint4& a, const uint4& b) {
     const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
@@ -1074,14 +1079,19 @@ constexpr uint32_t kMidLdsMax = 8192u;    // LDS-staged values up to here, in pl
 constexpr uint32_t kPrefetch = 4u;        // output chunks per lane: 4096 / 16 / 64
 
 // Stages value bytes g[0 .. n) into LDS at offset 0 (16B-aligned), whatever
-// g's alignment: whole aligned 16-byte loads (an aligned chunk never crosses a
-// page, so the over-read cannot fault), realigned in registers.
+// g's alignment: whole aligned 16-byte loads of the chunks that hold value
+// bytes (such a chunk never crosses a page, so the over-read cannot fault; the
+// funnel's second chunk is loaded only when it holds one too), realigned in
+// registers.
 __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint8_t* lds) {
   const uint32_t head = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 15u);
   const uint4* base = reinterpret_cast<const uint4*>(g - head);
   const uint32_t chunks = (n + 15u) >> 4;
+  const uint32_t end = head + n;                 // chunk k holds value bytes iff 16 k < end
   uint4* l = reinterpret_cast<uint4*>(lds);
-  for (uint32_t c = lane_id(); c < chunks; c += 64u) l[c] = head ? funnel16(base[c], base[c + 1u], head) : base[c];
+  for (uint32_t c = lane_id(); c < chunks; c += 64u)
+    l[c] = head ? funnel16(base[c], 16u * (c + 1u) < end ? base[c + 1u] : make_uint4(0u, 0u, 0u, 0u), head)
+                : base[c];
 }
 
 // kFrame = false: LZ4_compress_limitedOutput per value; ret[v] = size or 0,
