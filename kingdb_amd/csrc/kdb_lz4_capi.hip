@@ -464,11 +464,11 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   s->ensure_running();
   const auto t0 = std::chrono::steady_clock::now();
   uint64_t done = 0;
-  // a short decode result comes back in the slot's reply (service.h), ahead of
+  // a short result (decode or compress) comes back in the slot's reply (service.h), ahead of
   // the done word: taken when both tags are this request's and the checksum
   // of its 108 data bytes matches
   SvcReply* rp =
-      (uint32_t)k < kSvcPostSlots && kind == kSvcDecode && !s->no_reply ? &s->box->reply[k] : nullptr;
+      (uint32_t)k < kSvcPostSlots && !s->no_reply ? &s->box->reply[k] : nullptr;
   for (uint32_t spins = 1;; spins++) {
     if (rp && __atomic_load_n(&rp->tag0, __ATOMIC_ACQUIRE) == want) {
       SvcReply r;
