@@ -344,11 +344,18 @@ struct RingSrc {
   uint8_t* ring;        // LDS: kR + kMirror bytes, 16-byte aligned
   uint32_t hi;          // positions below hi are staged (the last kR of them are in the ring)
   __device__ __forceinline__ bool in(uint32_t i, uint32_t n) const { return i - (hi - kR) <= kR - n; }
+  // The fallback's load is waited for inside its branch (the compiler
+  // otherwise waits at the join, on every read: vmcnt(0), in order, so also
+  // for every earlier global store; measured neutral on 1 MiB parts, kept for
+  // reads that do fall back)
   __device__ __forceinline__ uint32_t u8(uint32_t i) const {
     uint32_t v = ring[i & (kR - 1u)];
     const bool ok = in(i, 1u);
     if (ballot(!ok)) {
-      if (!ok) v = g[i];
+      uint32_t gv = 0;
+      if (!ok) gv = g[i];
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      v = ok ? v : gv;
     }
     return v;
   }
@@ -356,7 +363,10 @@ struct RingSrc {
     uint32_t v = lds_rd32(ring, i & (kR - 1u));
     const bool ok = in(i, 4u);
     if (ballot(!ok)) {
-      if (!ok) v = *reinterpret_cast<const u32u*>(g + i);
+      uint32_t gv = 0;
+      if (!ok) gv = *reinterpret_cast<const u32u*>(g + i);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+      v = ok ? v : gv;
     }
     return v;
   }
