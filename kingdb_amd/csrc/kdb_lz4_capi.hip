@@ -281,7 +281,7 @@ SvcBox* device_inbox(int dev, hipStream_t st) {
     svc_wc_fence();
   }
   if (!ok) {
-    hipFree(d);
+    (void)hipFree(d);
     return nullptr;
   }
   return b;

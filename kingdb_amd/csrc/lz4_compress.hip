@@ -236,6 +236,12 @@ struct Table32T {
   __device__ Table32T(uint32_t* p) : off(lds_off(p)) {}
   __device__ Table32T() : off(0) {}
   __device__ __forceinline__ static uint32_t empty(uint32_t word0) { return word_tag(word0) << 20; }
+  __device__ __forceinline__ static uint32_t tag(uint32_t seq) { return word_tag(seq); }
+  // every entry empty: the 16 KiB at t (the table's base), as 16-byte stores
+  __device__ __forceinline__ static void clear(uint32_t* t, uint32_t word0) {
+    const uint32_t f = empty(word0);
+    for (uint32_t i = lane_id(); i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(t)[i] = make_uint4(f, f, f, f);
+  }
   // get + put with the tag; *maybe: the old entry's tag is tg (the lane is on)
   __device__ __forceinline__ uint32_t xchg_tagged(uint32_t h, uint32_t p, uint32_t tg, bool on, Slot& s,
                                                   bool& maybe) const {
@@ -246,6 +252,52 @@ struct Table32T {
   }
   // the entry as this lane read it (v, its position, is implied)
   __device__ __forceinline__ void restore(const Slot& s, uint32_t) const { ((lds_u32*)(uintptr_t)off)[s.h] = s.e; }
+};
+
+// The same tagged byU32 table in 12 KiB, for launches whose values are all at
+// most kTagMaxLen bytes: two planes, the positions' low halves (4096 x u16) and
+// one byte per entry of position bits 16-19 and a 4-bit tag (bits 16-19 of the
+// hash product).  With the 2 KiB ring next to it a wave needs 14.1 KiB of LDS
+// instead of 20.1: 11 waves per CU instead of 7, so KingDB's 1 MiB parts of a
+// batch (2 560 per GPU in `--workload big`) all run in one round.  The planes
+// are exchanged together as Table12's are (one ds_mskor_rtn each, in lane order).
+struct Table24T {
+  static constexpr bool kTagged = true;
+  static constexpr uint32_t kBytes = 8192u + 4096u;
+  uint32_t off;                         // the u16 plane; the byte plane at off + 8192
+  struct Slot { uint32_t h, e; };       // h: the index (| the off-lane bit); e: the old entry, 24 bits
+  __device__ Table24T(uint32_t* p) : off(lds_off(p)) {}
+  __device__ Table24T() : off(0) {}
+  __device__ __forceinline__ static uint32_t tag(uint32_t seq) { return ((seq * 2654435761u) >> 16) & 15u; }
+  // every entry empty: position 0 with position 0's tag
+  __device__ __forceinline__ static void clear(uint32_t* t, uint32_t word0) {
+    const uint32_t b = tag(word0) << 4, f = b * 0x01010101u;
+    for (uint32_t i = lane_id(); i < kBytes / 16u; i += 64u)
+      reinterpret_cast<uint4*>(t)[i] = i < 512u ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(f, f, f, f);
+  }
+  __device__ __forceinline__ uint32_t xchg_tagged(uint32_t h, uint32_t p, uint32_t tg, bool on, Slot& s,
+                                                  bool& maybe) const {
+    s.h = h | (on ? 0u : 0x8000u);      // an off lane: past the allocation (see Table12::xchg)
+    const uint32_t sl = (h & 1u) << 4, sb = (h & 3u) << 3;
+    const uint32_t al = off + ((s.h << 1) & ~3u), ab = off + 8192u + (s.h & ~3u);
+    uint32_t ol, ob;
+    asm volatile(
+        "ds_mskor_rtn_b32 %0, %2, %3, %4\n\t"
+        "ds_mskor_rtn_b32 %1, %5, %6, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(ol), "=&v"(ob)
+        : "v"(al), "v"(0xffffu << sl), "v"((p & 0xffffu) << sl), "v"(ab), "v"(0xffu << sb),
+          "v"(((p >> 16) | (tg << 4)) << sb)
+        : "memory");
+    const uint32_t lo = __builtin_amdgcn_ubfe(ol, sl, 16), by = __builtin_amdgcn_ubfe(ob, sb, 8);
+    s.e = lo | (by << 16);
+    maybe = on && (by >> 4) == tg;
+    return lo | ((by & 15u) << 16);
+  }
+  __device__ __forceinline__ void restore(const Slot& s, uint32_t) const {
+    ((lds_u16*)(uintptr_t)off)[s.h] = (uint16_t)s.e;
+    ((lds_u8*)(uintptr_t)(off + 8192u))[s.h] = (uint8_t)(s.e >> 16);
+  }
 };
 
 // The per-sequence register window (compress_block's kWin) for tagged byU32
@@ -334,10 +386,11 @@ __device__ __forceinline__ uint4 funnel16(const uint4& a, const uint4& b, uint32
 // ~10 G1 sequences.  The ring holds positions [hi - kR, hi) at ring + (p mod
 // kR), with a kMirror-byte copy of its first bytes after its end so a 4-byte
 // read never wraps.
-struct RingSrc {
+template <uint32_t kRingBytes>
+struct RingSrcT {
   static constexpr bool kUnclamped = false;   // compress_block clamps (the fallback reads global memory)
   static constexpr bool kWindow = false;
-  static constexpr uint32_t kR = KDB_LZ4_RING_BYTES, kMirror = 64u, kChunk = 1024u, kFront = KDB_LZ4_RING_FRONT;
+  static constexpr uint32_t kR = kRingBytes, kMirror = 64u, kChunk = 1024u, kFront = KDB_LZ4_RING_FRONT;
   typedef uint32_t __attribute__((aligned(1))) u32u;
   const uint8_t* g;
   uint32_t S;
@@ -423,6 +476,13 @@ struct RingSrc {
 #endif
   }
 };
+
+using RingSrc = RingSrcT<KDB_LZ4_RING_BYTES>;
+// the compact launch's ring (Table24T): 2 KiB, measured as fast as 4 KiB with the 16 KiB table
+#ifndef KDB_LZ4_COMPACT_RING
+#define KDB_LZ4_COMPACT_RING 2048u
+#endif
+using RingSrcC = RingSrcT<KDB_LZ4_COMPACT_RING>;
 
 // out chunk = bytes [sh, sh+16) of the 32 bytes (a, b); sh in 0..15 (uniform)
 __device__ __forceinline__ uint4 funnel16(const uint4& a, const uint4& b, uint32_t sh) {
@@ -976,7 +1036,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
         // entry as the sequential loop's get at this iteration reads it
         bool maybe = true;
         if constexpr (Tab::kTagged) {
-          refk = tab.xchg_tagged(h, pk, word_tag(seq), valid, slot, maybe);
+          refk = tab.xchg_tagged(h, pk, Tab::tag(seq), valid, slot, maybe);
           maybe = maybe && pk <= refk + kMaxDistance;
         } else {
           refk = tab.xchg(h, pk, valid, slot);
@@ -1025,7 +1085,7 @@ __device__ __forceinline__ int compress_block(Src& src, uint32_t S, const Tab& t
           uint32_t cw;
           if constexpr (Tab::kTagged) {
             bool maybe;
-            refk = tab.xchg_tagged(h, pk, word_tag(seq), valid, slot, maybe);
+            refk = tab.xchg_tagged(h, pk, Tab::tag(seq), valid, slot, maybe);
             cw = ~seq;
             if (maybe && pk <= refk + kMaxDistance) cw = RD32(refk);
           } else {
@@ -1350,7 +1410,9 @@ size_t compress_lds_bytes(uint32_t max_len) {
 // 1 MB (util/options.h:171), so whole parts land here.  The value is read in
 // place from global memory (L2), the 16 KiB table lives in LDS; one wave per
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
-template <bool kFrame, bool kWide>
+// kCompact (byU32 launches whose values are all at most kTagMaxLen bytes):
+// Table24T and the 2 KiB ring in 14.1 KiB of LDS.
+template <bool kFrame, bool kWide, bool kCompact = false>
 __device__ __forceinline__ void big_values(
     uint32_t* const tab32, uint8_t* const ring, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
@@ -1363,6 +1425,9 @@ __device__ __forceinline__ void big_values(
   if constexpr (kWide) tab = Table32(tab32);
   else tab = Table16(reinterpret_cast<uint16_t*>(tab32));
   const Table32T tabt(tab32);
+  const Table24T tabc(tab32);
+  static_assert(!kCompact || kWide, "the compact table is byU32's");
+  if constexpr (kCompact) max_len = min(max_len, kTagMaxLen);   // every value tagged
   bool direct_done = false;
 #pragma unroll 1
   for (;;) {
@@ -1391,8 +1456,12 @@ __device__ __forceinline__ void big_values(
       // byU32 values of at most kTagMaxLen bytes (KingDB's 1 MB parts) take the
       // tagged table, whose empty entries hold position 0's tag
       const bool tagged = kWide && S <= kTagMaxLen && S >= 4u;
-      const uint32_t fill = tagged ? Table32T::empty(uni(*reinterpret_cast<const GlobalSrc::u32u*>(g))) : 0u;
-      for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(fill, fill, fill, fill);
+      if constexpr (kCompact) {
+        Table24T::clear(tab32, uni(*reinterpret_cast<const GlobalSrc::u32u*>(g)));
+      } else {
+        const uint32_t fill = tagged ? Table32T::empty(uni(*reinterpret_cast<const GlobalSrc::u32u*>(g))) : 0u;
+        for (uint32_t i = lane; i < 4096u / 4u; i += 64u) reinterpret_cast<uint4*>(tab32)[i] = make_uint4(fill, fill, fill, fill);
+      }
       const uint32_t bound = compress_bound(S);                   // 0 past LZ4_MAX_INPUT_SIZE
       GlobalSrc ws{g, S, 0u};
       // compress_block over the value with source R and table T (cap: the
@@ -1402,7 +1471,10 @@ __device__ __forceinline__ void big_values(
                        : compress_block<kWide, false>(rsrc, S, t, o + skip, b, cap);
       };
       auto run_any = [&](uint32_t skip, int cap, int b) -> int {
-        if constexpr (kWide) {
+        if constexpr (kCompact) {
+          RingSrcC rs{g, S, ring, 0u, {}, {}, false};
+          return run(rs, tabc, skip, cap, b);
+        } else if constexpr (kWide) {
           if (tagged) {
 #if KDB_LZ4_WIDE_RING
             RingSrc rs{g, S, ring, 0u, {}, {}, false};
@@ -1464,6 +1536,23 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t ring[kWide && KDB_LZ4_WIDE_RING ? RingSrc::kR + RingSrc::kMirror : 16u];
   big_values<kFrame, kWide>(tab32, ring, src, src_off, src_len, n, min_len, max_len, dst, dst_off, dst_cap, frame_len,
                             ret, work, batch);
+}
+
+// byU32 launches whose values are all at most kTagMaxLen bytes (KingDB's 1 MiB
+// parts): Table24T + the 2 KiB ring, 12 + 2.06 KiB: 11 waves per CU (LDS)
+template <bool kFrame>
+__global__ __launch_bounds__(64) void lz4_compress_big_compact_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
+    uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
+    uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
+    const uint32_t* __restrict__ census, uint32_t cls, uint32_t prio) {
+  if (census && census[cls] == 0) return;
+  if (prio) __builtin_amdgcn_s_setprio(2);
+  __shared__ __attribute__((aligned(16))) uint32_t tab[Table24T::kBytes / 4u];
+  __shared__ __attribute__((aligned(16))) uint8_t ring[RingSrcC::kR + RingSrcC::kMirror];
+  big_values<kFrame, true, true>(tab, ring, src, src_off, src_len, n, min_len, max_len, dst, dst_off, dst_cap, frame_len,
+                                 ret, work, batch);
 }
 
 // A batch with values on both sides of 4 KiB .. 8 KiB (a mixed batch): ONE
@@ -1558,14 +1647,18 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
                              uint32_t n, uint32_t min_len, uint32_t max_len, uint8_t* dst, const uint64_t* dst_off,
                              const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret,
                              const uint32_t* census = nullptr, uint32_t cls = 0) {
-  auto kern = lz4_compress_big_kernel<F, W>;
+  // byU32 values all within the tagged table's reach: the compact kernel
+  static const bool compact_on = kdb_tune("KDB_LZ4_COMPACT", 1) != 0;   // 0: the 16 KiB table (A/B)
+  const bool compact = W && compact_on && max_len <= kTagMaxLen;
+  auto kern = compact ? lz4_compress_big_compact_kernel<F> : lz4_compress_big_kernel<F, W>;
   static const uint32_t prio = env_prio();
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
   uint32_t* work = nullptr;
   hipError_t e = launch_counter(st, n, grid, &work);
   if (e != hipSuccess) return e;
   const uint32_t batch = work ? claim_batch(n, grid) : 1u;   // values per claim; lanes >= batch idle
-  launch_note(F ? (W ? "lz4_compress_big_kernel<true, true>" : "lz4_compress_big_kernel<true, false>")
+  launch_note(compact ? (F ? "lz4_compress_big_compact_kernel<true>" : "lz4_compress_big_compact_kernel<false>")
+              : F ? (W ? "lz4_compress_big_kernel<true, true>" : "lz4_compress_big_kernel<true, false>")
                 : (W ? "lz4_compress_big_kernel<false, true>" : "lz4_compress_big_kernel<false, false>"));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, min_len, max_len, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, prio);
@@ -1659,15 +1752,19 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
       if (r != hipSuccess) return r;
     }
     if (on[3]) {
-      r = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
+      // the caller's max_len bounds this class's values (the compact kernel's
+      // test).  Host code takes no min() here: HIP's host min() on uint32_t is
+      // the signed one (min(x, 0xFFFFFFFFu) == 0xFFFFFFFFu)
+      const uint32_t top = max_len < hi[3] ? max_len : hi[3];
+      r = frame ? launch_big<true, true>(aux, src, src_off, src_len, n, lo[3], top, dst, dst_off, dst_cap,
                                          frame_len, ret, census, 3)
-                : launch_big<false, true>(aux, src, src_off, src_len, n, lo[3], hi[3], dst, dst_off, dst_cap,
+                : launch_big<false, true>(aux, src, src_off, src_len, n, lo[3], top, dst, dst_off, dst_cap,
                                           frame_len, ret, census, 3);
       if (r != hipSuccess) return r;
     }
     if (on[0] && !combo) {
       const size_t lds = 0;   // static LDS (compress_lds_bytes(kSmallMax) bytes)
-      const uint32_t guide = claim_guide(min(max_len, kSmallMax));
+      const uint32_t guide = claim_guide(max_len < kSmallMax ? max_len : kSmallMax);
       // batched emission when the launch may hold values of kBatchMin bytes
       // and more (a launch of short values only keeps the per-sequence form)
       const bool bat = max_len >= kBatchMin;
@@ -1685,7 +1782,7 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
     // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
     if (on[1]) {
-      const uint32_t top = min(max_len, hi[1]);
+      const uint32_t top = max_len < hi[1] ? max_len : hi[1];   // (host min() is signed)
       const size_t lds = compress_lds_bytes(top);
       r = frame ? launch_one<true, false, kEmitBatch>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
                                                       dst_cap, frame_len, ret, census, 1, claim_guide(top))

@@ -254,8 +254,9 @@ def decompress_blocks(blocks: list[bytes], sizes: list[int], targets: list[int] 
     return res
 
 
-def compress_frames(values: list[bytes]) -> list[bytes]:
-    """CompressorLZ4::Compress per value (one launch); raises on IOError."""
+def compress_frames(values: list[bytes], max_len: int | None = None) -> list[bytes]:
+    """CompressorLZ4::Compress per value (one launch); raises on IOError.
+    max_len: the launch's bound on the values' lengths (default: the largest)."""
     n = len(values)
     if n == 0:
         return []
@@ -274,8 +275,8 @@ def compress_frames(values: list[bytes]) -> list[bytes]:
     meta.upload(m)
     b = meta.ptr
     _lib.check(lib().kdb_lz4_compress_frames_batch(
-        None, d_src.ptr, b, b + 8 * n, n, int(lens.max()), d_dst.ptr, b + 12 * n, b + 20 * n, b + 24 * n),
-        "compress_frames_batch")
+        None, d_src.ptr, b, b + 8 * n, n, int(lens.max()) if max_len is None else max_len, d_dst.ptr, b + 12 * n,
+        b + 20 * n, b + 24 * n), "compress_frames_batch")
     out = d_dst.download()
     md = meta.download(8 * n, 20 * n)
     flen = md[: 4 * n].view(np.uint32)

@@ -353,10 +353,29 @@ def test_byu32_tagged_table_edges(gpu, orc):
     # a value repeated whole, 150 000 bytes back (past the window)
     z = bytearray(rng.integers(0, 256, 300000, dtype=np.uint8).tobytes())
     vals.append(bytes(z[:150000]) * 2)
+    want = [orc.frame(v) for v in vals]
     frames = gpu.compress_frames(vals)
-    assert frames == [orc.frame(v) for v in vals]
+    assert frames == want
     back = gpu.decompress_frames(frames, [len(v) for v in vals])
     assert all(st == 0 and out == v for (st, out), v in zip(back, vals))
+    # the same values of at most 1 MiB alone: a launch whose max_len is within the
+    # tag limit takes the compact kernel (Table24T: 4-bit tags, position bits 16-19
+    # in the byte plane, the 2 KiB ring)
+    le = [i for i, v in enumerate(vals) if len(v) <= 1 << 20]
+    assert gpu.compress_frames([vals[i] for i in le]) == [want[i] for i in le]
+
+
+def test_compress_max_len_unbounded(gpu, orc):
+    """max_len is a bound, not the exact largest length: 0xFFFFFFFF (a caller that
+    does not know its lengths) gives the same frames for every size class.  Host
+    code once took HIP's host min(), which is signed on uint32_t, and failed the
+    4-8 KiB class's launch for bounds of 2^31 and more."""
+    pool = oracle.g1_pool(orc)
+    vals = (oracle.g1_values(pool, 100, 3) + oracle.g1_values(pool, 6000, 2) + oracle.g1_values(pool, 30000, 2)
+            + oracle.g1_values(pool, 200000, 1))
+    want = [orc.frame(v) for v in vals]
+    for bound in (0xFFFFFFFF, 1 << 31, (1 << 20) + 1):
+        assert gpu.compress_frames(vals, max_len=bound) == want, bound
 
 
 def test_big_scalar_mirrors(gpu, orc):
