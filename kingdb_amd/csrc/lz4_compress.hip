@@ -258,9 +258,17 @@ struct Table32T {
 // most kTagMaxLen bytes: two planes, the positions' low halves (4096 x u16) and
 // one byte per entry of position bits 16-19 and a 4-bit tag (bits 16-19 of the
 // hash product).  With the 2 KiB ring next to it a wave needs 14.1 KiB of LDS
-// instead of 20.1: 11 waves per CU instead of 7, so KingDB's 1 MiB parts of a
-// batch (2 560 per GPU in `--workload big`) all run in one round.  The planes
-// are exchanged together as Table12's are (one ds_mskor_rtn each, in lane order).
+// instead of 20.1: 10 waves per CU instead of 7 (tools/probe/lds_occupancy --
+// the hardware admits 10 workgroups of 14.1 or 15 KiB per CU but only 9 of
+// 16 KiB, and 7 of 20.1), so KingDB's 1 MiB parts of a batch (2 560 per GPU in
+// `--workload big`) all run in one round: compress 14.2 -> 11.15 ms.  The
+// planes are exchanged together as Table12's are (one ds_mskor_rtn each, in
+// lane order).  Per wave it is slower than Table32T (at 7 waves per CU, ~9.4
+// against 7.1 ms per round: 1 in 16 stale far entries pass a 4-bit tag and cost
+// a global read each), and more tag bits measured no better overall
+// (profiles/r05/r05_c*: a 6-bit tag in a third, 2-bit plane 11.3 ms -- one more
+// LDS atomic per exchange; an 8-bit tag in 14 KiB needs 16 KiB with the ring,
+// 9 waves per CU, 17.2 ms; the same with a 1 KiB ring 17.6-19.9 ms).
 struct Table24T {
   static constexpr bool kTagged = true;
   static constexpr uint32_t kBytes = 8192u + 4096u;
@@ -1411,7 +1419,7 @@ size_t compress_lds_bytes(uint32_t max_len) {
 // place from global memory (L2), the 16 KiB table lives in LDS; one wave per
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
 // kCompact (byU32 launches whose values are all at most kTagMaxLen bytes):
-// Table24T and the 2 KiB ring in 14.1 KiB of LDS.
+// Table24T and the 2 KiB ring in 14.1 KiB of LDS (10 waves per CU).
 template <bool kFrame, bool kWide, bool kCompact = false>
 __device__ __forceinline__ void big_values(
     uint32_t* const tab32, uint8_t* const ring, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -1539,7 +1547,8 @@ __global__ __launch_bounds__(64) void lz4_compress_big_kernel(
 }
 
 // byU32 launches whose values are all at most kTagMaxLen bytes (KingDB's 1 MiB
-// parts): Table24T + the 2 KiB ring, 12 + 2.06 KiB: 11 waves per CU (LDS)
+// parts): Table24T + the 2 KiB ring, 12 + 2.06 KiB: 10 waves per CU (LDS;
+// hipOccupancy says 11, the hardware admits 10: tools/probe/lds_occupancy)
 template <bool kFrame>
 __global__ __launch_bounds__(64) void lz4_compress_big_compact_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
