@@ -68,7 +68,9 @@ def test_last_kernels_names(gpu):
     assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u>", "lz4_compress_kernel<true, false, 1u>"]
     K.compress_frames([b"x" * 4096, b"y" * 20000])
     assert K.last_kernels() == ["lz4_compress_mixed_kernel<true>", "lz4_compress_kernel<true, false, 1u>"]
-    K.compress_frames([b"x" * 100000])
+    K.compress_frames([b"x" * 100000])                  # byU32, every value <= 1 MiB: the compact table
+    assert "lz4_compress_big_compact_kernel<true>" in K.last_kernels()
+    K.compress_frames([b"x" * 100000, b"z" * ((1 << 20) + 1)])
     assert "lz4_compress_big_kernel<true, true>" in K.last_kernels()
     K.decompress_frames(K.compress_frames([b"x" * 4096] * 4), [4096] * 4)
     assert K.last_kernels() == ["lz4_decompress_kernel<true, 3u>"]     # every frame <= 3 057 B

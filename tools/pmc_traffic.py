@@ -78,7 +78,7 @@ def main():
         # classes (big / mixed kernels) also gather 4-byte candidate words and the
         # ring decoder refills with dword loads: for them the true read bytes lie
         # between the raw count and twice it, and both are reported.
-        narrow = any(t in nm for t in ("big_kernel", "mixed_kernel", "mixed24_kernel"))
+        narrow = any(t in nm for t in ("big_kernel", "big_compact_kernel", "mixed_kernel", "mixed24_kernel"))
         res["kernels"][k] = {
             "kernel": nm, "fetch_size_kib_raw": f, "write_size_kib_raw": w,
             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
