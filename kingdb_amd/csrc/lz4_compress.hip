@@ -1793,9 +1793,15 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     if (on[1]) {
       const uint32_t top = max_len < hi[1] ? max_len : hi[1];   // (host min() is signed)
       const size_t lds = compress_lds_bytes(top);
-      r = frame ? launch_one<true, false, kEmitBatch>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
+      // Beside a byU32 launch this class queues behind it on aux: its 24 KiB
+      // workgroups cannot start while the byU32 waves hold the CUs' LDS, and
+      // waiting in the dispatcher next to them they cost the byU32 launch
+      // 1.4 ms even with no value of their own (1 MiB parts: compress 12.6 ->
+      // 11.1 ms without the fork, profiles/r05/r05_nf_*)
+      hipStream_t s1 = on[3] ? aux : st;
+      r = frame ? launch_one<true, false, kEmitBatch>(s1, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
                                                       dst_cap, frame_len, ret, census, 1, claim_guide(top))
-                : launch_one<false, false, kEmitBatch>(st, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
+                : launch_one<false, false, kEmitBatch>(s1, lds, src, src_off, src_len, n, lo[1], top, dst, dst_off,
                                                        dst_cap, frame_len, ret, census, 1, claim_guide(top));
     }
     return r;
