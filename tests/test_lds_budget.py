@@ -1,0 +1,52 @@
+"""LDS budgets the occupancy of the latency-bound kernels depends on (no GPU).
+
+The hardware allocates a workgroup's LDS in 1 280-byte steps out of 160 KiB
+(tools/probe/lds_occupancy.hip; every size probed on MI355X fits that rule,
+profiles/r05/r05_occ.txt), so a kernel holds floor(163840 / ceil(lds / 1280) /
+1280) one-wave workgroups per CU -- fewer than hipOccupancy... predicts for
+sizes just over a step.  The compact byU32 compressor exists to hold all of a
+batch's 2 560 1 MiB parts in one round (10 per CU); this test
+reads the compiler's resource report and fails when its LDS grows past that.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIPCC = "/opt/rocm/bin/hipcc"
+STEP, TOTAL = 1280, 163840
+
+
+def resident(lds: int) -> int:
+    return TOTAL // (-(-lds // STEP) * STEP) if lds else 64
+
+
+def test_step_rule_matches_probe():
+    """The rule against the probe's measurements (r05_occ.txt)."""
+    for lds, want in ((16384, 9), (16256, 9), (16000, 9), (15360, 10), (14400, 10), (20544, 7), (12800, 12),
+                      (24576, 6), (6400, 25), (6656, 21), (7264, 21)):
+        assert resident(lds) == want, lds
+
+
+@pytest.mark.skipif(not shutil.which(HIPCC) and not os.path.exists(HIPCC), reason="hipcc absent")
+def test_compact_kernel_holds_ten_per_cu():
+    csrc = os.path.join(ROOT, "kingdb_amd", "csrc")
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                        "-I" + csrc, "-Rpass-analysis=kernel-resource-usage", "-c",
+                        os.path.join(csrc, "lz4_compress.hip"), "-o", os.devnull],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lds, name = {}, None
+    for line in r.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.search(r"LDS Size \[bytes/block\]: (\d+)", line)
+        if m and name:
+            lds[name] = int(m.group(1))
+    compact = [v for k, v in lds.items() if "big_compact_kernel" in k]
+    assert compact, sorted(lds)
+    assert all(resident(v) >= 10 for v in compact), compact
