@@ -63,6 +63,14 @@ int kdb_lz4_service_stats(int device, uint32_t* launches, uint32_t* served, uint
  * input read with the doorbells, no second PCIe round trip), and decode
  * results answered by a reply record ahead of the done word (service.h). */
 int kdb_lz4_service_counters(int device, uint32_t* polls, uint32_t* from_post, uint32_t* replied);
+/* Test hook for the services' request numbers (kdb_lz4_capi.hip,
+ * service_call): on the calling thread's device, stops each service created
+ * so far, waits for its wave to leave, and sets every slot as if its last
+ * request had been number `req` (doorbell, the host's copy, the done word),
+ * with a reply record of tags `reply_tag`, return value 0 and a valid
+ * checksum (a record a wave wrote `reply_tag` requests ago).  The next call
+ * on a slot then takes request number req + 1, skipping 0. */
+int kdb_lz4_service_seed_requests(uint32_t req, uint32_t reply_tag);
 /* The kernels (rocprof names, ';'-separated) that the calling thread's last
  * compress or decompress batch queued.  No HIP call. */
 int kdb_lz4_last_kernels(char* buf, uint64_t cap);

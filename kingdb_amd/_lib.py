@@ -36,6 +36,7 @@ SIGNATURES = {
     "kdb_lz4_selftest": (_i, [_i, _c.POINTER(_i), _c.POINTER(_u32)]),
     "kdb_lz4_service_stats": (_i, [_i, _c.POINTER(_u32), _c.POINTER(_u32), _c.POINTER(_u32)]),
     "kdb_lz4_service_counters": (_i, [_i, _c.POINTER(_u32), _c.POINTER(_u32), _c.POINTER(_u32)]),
+    "kdb_lz4_service_seed_requests": (_i, [_u32, _u32]),
     "kdb_lz4_last_kernels": (_i, [_c.c_char_p, _u64]),
     "kdb_lz4_build_id": (_i, [_c.c_char_p, _u64]),
     "kdb_lz4_max_u32": (_i, [_vp, _vp, _u32, _vp]),

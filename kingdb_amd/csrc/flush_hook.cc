@@ -233,6 +233,10 @@ struct ThreadPipe {
   bool lane_set = false;
 };
 std::atomic<uint64_t> g_pipeline_ids{1};
+// ids of the pipelines alive now: a client thread's per-pipeline records
+// (Pipeline::thread_pipe) of closed databases are dropped against it
+std::mutex g_live_mu;
+std::unordered_set<uint64_t> g_live_ids;
 // KDB_LZ4_FLUSH_STATS: when WriteBuffer::WritePart accounted this thread's last
 // deferred chunk (its lock and buffer-full wait come after that point)
 thread_local std::chrono::steady_clock::time_point t_accounted;
@@ -336,6 +340,10 @@ constexpr uint64_t kLaneSpan = 2ull << 20;
 class Pipeline {
  public:
   explicit Pipeline(int device) : device_(device) {
+    {
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live_ids.insert(id_);
+    }
     // the lanes: this thread's device (the one the caller bound with
     // kdb_lz4_set_device) only, by default -- in a deployment of one process
     // per GPU no process touches another's device; KDB_LZ4_FLUSH_DEVICES=<n>
@@ -359,6 +367,10 @@ class Pipeline {
     if (ws > 0) watch_ = std::thread(&Pipeline::watch, this, ws);
   }
   ~Pipeline() {
+    {
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live_ids.erase(id_);
+    }
     const Clock::time_point t0 = Clock::now();
     {
       std::lock_guard<std::mutex> l(mu_);
@@ -556,6 +568,11 @@ class Pipeline {
     thread_local ThreadPipe* last = nullptr;
     if (last_id == id_ && last) return *last;
     thread_local std::unordered_map<uint64_t, ThreadPipe> all;
+    if (all.find(id_) == all.end() && !all.empty()) {
+      // a thread that outlives many databases keeps records of the open ones only
+      std::lock_guard<std::mutex> l(g_live_mu);
+      for (auto it = all.begin(); it != all.end();) it = g_live_ids.count(it->first) ? std::next(it) : all.erase(it);
+    }
     last = &all[id_];      // node-based: the reference stays valid across inserts
     last_id = id_;
     return *last;
@@ -1208,11 +1225,26 @@ void LZ4FlushOrders(const void* wb, const DatabaseOptions& db_options, std::vect
   if (p) p->complete(orders);
 }
 
+// The write buffer's constructor (the thread opening the database): the entry
+// for this address is the new buffer's from now on, whatever a closed buffer
+// at the same address left in g_closed.
+void LZ4FlushOpen(const void* wb, const DatabaseOptions& db_options) {
+  {
+    std::lock_guard<std::mutex> l(g_mu);
+    g_closed.erase(wb);
+  }
+  if (LZ4FlushDeferrable(db_options)) pipeline_of(wb, true);
+}
+
 LZ4FlushScope::LZ4FlushScope(const void* wb, const DatabaseOptions& db_options) : wb_(wb) {
 #ifdef KDB_LZ4_HANG_DUMP
   signal(SIGUSR2, kdb_dump_one);
   signal(SIGUSR1, kdb_dump_all);
 #endif
+  // test knob: a ProcessingLoop thread that the scheduler starts late (the
+  // put loop of the database that was just opened runs meanwhile)
+  if (const char* d = getenv("KDB_LZ4_FLUSH_SCOPE_DELAY_US"))
+    std::this_thread::sleep_for(std::chrono::microseconds(strtoul(d, nullptr, 10)));
   {
     std::lock_guard<std::mutex> l(g_mu);
     g_closed.erase(wb);

@@ -430,7 +430,18 @@ bool service_call(int kind, const char* source, uint32_t in_len, char* dest, uin
   SvcSlot& sl = s->box->slot[k];
   // the request number: from the host's copy (the inbox may be device memory,
   // whose reads cross PCIe)
-  const uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
+  uint32_t want = __atomic_load_n(&s->box->req[k], __ATOMIC_RELAXED) + 1u;
+  if (want == 0u) {
+    // 2^32 calls on this slot: 0 is never a request number (a zero-filled reply
+    // record or done word would pass for its answer), and a reply record
+    // written one wrap ago may carry any tag, so its tags are cleared (the
+    // slot's previous request is answered: the wave writes nothing here now)
+    want = 1u;
+    if ((uint32_t)k < kSvcPostSlots) {
+      __atomic_store_n(&s->box->reply[k].tag0, 0u, __ATOMIC_RELAXED);
+      __atomic_store_n(&s->box->reply[k].tag1, 0u, __ATOMIC_RELAXED);
+    }
+  }
   if ((uint32_t)k < kSvcPostSlots) {
     // the post: arguments and (up to kSvcPostInline bytes) the input, the
     // checksum and both tags, built here and written whole (service.h)
@@ -719,6 +730,42 @@ int kdb_lz4_device_sync(void) {
     s->mu.unlock();
   }
   return hip_status(e);
+}
+int kdb_lz4_service_seed_requests(uint32_t req, uint32_t reply_tag) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_status(e);
+  std::vector<Service*> held;
+  {
+    std::lock_guard<std::mutex> l(g_svc_mu);
+    for (int kind = 0; kind < 2; kind++)
+      for (int w = 0; w < kSvcWavesMax; w++) {
+        const size_t at = svc_index(dev, kind, w);
+        Service* s = at < services().size() ? services()[at] : nullptr;
+        if (s && s->ok) held.push_back(s);
+      }
+  }
+  for (Service* s : held) {
+    std::lock_guard<std::mutex> l(s->mu);
+    __atomic_store_n(&s->in->stop, 1u, __ATOMIC_SEQ_CST);
+    svc_wc_fence();
+    e = hipStreamSynchronize(s->stream);   // the wave has left
+    __atomic_store_n(&s->in->stop, 0u, __ATOMIC_SEQ_CST);
+    if (e != hipSuccess) return hip_status(e);
+    for (uint32_t k = 0; k < kSvcSlots; k++) {
+      __atomic_store_n(&s->in->req[k], req, __ATOMIC_RELAXED);
+      __atomic_store_n(&s->box->req[k], req, __ATOMIC_RELAXED);
+      __atomic_store_n(&s->box->done[k], (uint64_t)req << 32, __ATOMIC_RELAXED);
+      if (k < kSvcPostSlots) {
+        SvcReply& r = s->box->reply[k];
+        memset(&r, 0, sizeof(r));   // zero data: checksum 0
+        r.tag0 = r.tag1 = reply_tag;
+      }
+    }
+    svc_wc_fence();
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
+  return KDB_LZ4_OK;
 }
 int kdb_lz4_event_create(void** event) {
   return event ? hip_status(hipEventCreate((hipEvent_t*)event)) : KDB_LZ4_EINVAL;

@@ -72,6 +72,15 @@ uint64_t LZ4FlushAccount(uint64_t chunk_size);
 // stored.  Never aborts.
 void LZ4FlushOrders(const void* wb, const DatabaseOptions& db_options, std::vector<Order>& orders);
 
+// WriteBuffer's constructor, on the thread that opens the database, before
+// ProcessingLoop starts: creates the pipeline, so it exists before Open()
+// returns and the first put can reach LZ4FlushDefer.  (Created only by
+// ProcessingLoop's LZ4FlushScope, a put that came before that thread ran found
+// the address of the previous, closed write buffer -- the allocator hands the
+// same address to the next WriteBuffer -- and was refused as "closing":
+// test_db's SingleThreadSmallEntriesCompaction)
+void LZ4FlushOpen(const void* wb, const DatabaseOptions& db_options);
+
 // ProcessingLoop's local: creates the pipeline (GPU stream, staging, worker
 // thread) when the write buffer starts, and drains and stops it when the loop
 // returns (WriteBuffer::Close).

@@ -130,6 +130,16 @@ EDITS = {
          "  bool has_data;\n"
          "  bool notified_ = false;   // NotifyWait() was called (hook build)\n"),
     ],
+    # The pipeline is created on the thread that opens the database, before
+    # ProcessingLoop's thread starts: a put that came before that thread ran
+    # found only the previous (closed) write buffer's entry at the same address
+    # and was refused.
+    "cache/write_buffer.h": [
+        ('#include "thread/event_manager.h"\n', '#include "thread/event_manager.h"\n' + INCLUDE),
+        ("    thread_buffer_handler_ = std::thread(&WriteBuffer::ProcessingLoop, this);\n",
+         "    LZ4FlushOpen(this, db_options_);   // the pipeline exists before Open() returns\n"
+         "    thread_buffer_handler_ = std::thread(&WriteBuffer::ProcessingLoop, this);\n"),
+    ],
     "interface/database.cc": [
         ('#include "interface/database.h"\n', '#include "interface/database.h"\n' + INCLUDE),
         ("  bool do_compression = true;\n  uint64_t size_value_compressed = 0;\n",

@@ -191,3 +191,25 @@ def test_service_stress_threads(gpu, busy):
     r = subprocess.run([exe, "8", "300", "7", str(busy)], cwd=ROOT, capture_output=True, text=True, timeout=240,
                        env=dict(os.environ, KDB_ORACLE_SO=os.path.join(ROOT, "oracle", "liblz4_oracle.so")))
     assert r.returncode == 0 and "ok:" in r.stdout, (r.stdout[-1000:], r.stderr[-3000:])
+
+
+def test_service_request_numbers_wrap(gpu, orc):
+    """A slot's request number wraps after 2^32 calls: 0 is never
+    used (a zero-filled reply record or done word would pass for its answer),
+    and a reply record left from the previous wrap cannot be taken for the
+    first requests after it.  kdb_lz4_service_seed_requests puts every slot
+    just before the wrap, with reply records of tag 0 (never written) and then
+    of tag 1 (written one wrap ago), each with a valid checksum and return 0."""
+    from kingdb_amd import _lib
+    lib = _lib.load()
+    pool = oracle.g1_pool(orc)
+    vals = oracle.g1_values(pool, 100, 8)
+    blocks = [orc.compress(v) for v in vals]
+    for v, b in zip(vals, blocks):   # the services exist, this thread holds its slots
+        assert gpu.decompress_safe_partial(b, len(v), len(v)) == (len(v), v)
+        assert gpu.compress_limited_output(v, orc.compress_bound(len(v))) == (len(b), b)
+    for req, tag in ((0xFFFFFFFF, 0), (0xFFFFFFFE, 1), (0xFFFFFFFD, 2)):
+        assert lib.kdb_lz4_service_seed_requests(ctypes.c_uint32(req), ctypes.c_uint32(tag)) == 0
+        for v, b in zip(vals, blocks):   # numbers req+1, ... across the wrap
+            assert gpu.decompress_safe_partial(b, len(v), len(v)) == (len(v), v), (hex(req), tag)
+            assert gpu.compress_limited_output(v, orc.compress_bound(len(v))) == (len(b), b), (hex(req), tag)
