@@ -117,9 +117,11 @@ uint32_t services_resident(int dev);   // kdb_lz4_capi.hip (service.h)
 // Workgroups of 64 threads resident at once for `kern` with `lds` bytes of
 // dynamic LDS, capped at n (the kernels dequeue values dynamically, so a
 // workgroup that is admitted late simply takes fewer values).
-uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
+// `waves` > 1: workgroups of that many waves (one value each at a time), at
+// most ceil(n / waves) of them.
+uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n, uint32_t waves) {
   int per_cu = 0, dev = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds) != hipSuccess || per_cu < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * (int)waves, lds) != hipSuccess || per_cu < 1)
     per_cu = 1;
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
@@ -133,9 +135,12 @@ uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n) {
   // for as long as calls keep coming: a grid that counted on that CU's full
   // capacity would leave a workgroup waiting behind it, and the launch's tail
   // with it, so each one resident on this device takes a margin off the grid
+  // (a workgroup of several waves waits for a whole CU's worth: one per wave)
   const uint32_t svc = services_resident(dev);
-  if (svc) slots = slots > 8u * svc + 1u ? slots - 8u * svc : 1u;
-  return (uint32_t)(n < slots ? n : slots);
+  const uint64_t margin = waves > 1 ? svc : 8u * svc;
+  if (svc) slots = slots > margin + 1u ? slots - margin : 1u;
+  const uint32_t groups = waves > 1 ? (uint32_t)(((uint64_t)n + waves - 1u) / waves) : n;
+  return (uint32_t)(groups < slots ? groups : slots);
 }
 
 // Fork/join of a second stream, so that size-class launches overlap: the

@@ -122,8 +122,20 @@ constexpr uint32_t kT12Lo = KDB_T12_LO, kT12Hi = KDB_T12_HI;
 static_assert(kT12Lo == 4096u && kT12Hi == kT12Lo + 8192u, "value, then the 8 KiB low-byte plane, then the nibbles");
 #define KDB_STR2(x) #x
 #define KDB_STR(x) KDB_STR2(x)
-struct Table12 {
+// An off lane's address bits in a workgroup of several waves, each with its
+// 16 KiB region at base = wave x 16 KiB (lz4_compress_kernel<..., kWaves>):
+// 163 840, the whole 160 KiB past LDS address 0, so `base | h` for an off
+// lane lands past the workgroup's allocation from every wave's region (its
+// bits, 15 and 17, are clear in every slot index and nibble address).
+constexpr uint32_t kOffLaneWG = 0x28000u;
+// kBased: the table of wave `base >> 14` of a multi-wave workgroup -- its
+// planes at base + kT12Lo / base + kT12Hi.  The base rides in the off-lane
+// select the exchange makes anyway (on ? base : kOffLaneWG), so no address
+// of the parse carries an add for it.
+template <bool kBased>
+struct Table12T {
   static constexpr bool kTagged = false;
+  uint32_t base = 0;   // kBased: this wave's region (a multiple of 16 KiB)
   // a lane's slot as the exchange addressed it, kept for restore(): the low
   // byte's index, the high nibble's dword address (in its plane) and shift
   struct Slot { uint32_t lo, hi, sh, mh; };
@@ -136,7 +148,7 @@ struct Table12 {
     // restore is dropped too) instead of carrying a zero mask and zero data:
     // one select for the address instead of four on the masks and data
     // (compress 9.07 -> 9.00 ms, profiles/r04_d/r04_e_ab_exchange_oor.txt)
-    const uint32_t oor = on ? 0u : 0x10000u;
+    const uint32_t oor = kBased ? (on ? base : kOffLaneWG) : (on ? 0u : 0x10000u);
     s.lo = h | oor;
     s.hi = ((h >> 1) & ~3u) | oor;
     const uint32_t ml = 0xffu << sl;
@@ -171,6 +183,7 @@ struct Table12 {
                  : "memory");
   }
 };
+using Table12 = Table12T<false>;
 constexpr uint32_t kTable12Bytes = 8192u + 4096u;
 // The off-lane addresses of the exchanges (Table12/16/32::xchg) rely on the
 // hardware dropping LDS accesses past the kernel's allocation: they start at
@@ -1188,7 +1201,16 @@ __device__ __forceinline__ void stage_aligned(const uint8_t* g, uint32_t n, uint
 // goes), kEmitBatch (batched), or kEmitPerValue (two instances of the parse,
 // batched for values of kBatchMin bytes and more).
 constexpr uint32_t kEmitDirect = 0, kEmitBatch = 1, kEmitPerValue = 2;
-template <bool kFrame, bool kSmall, uint32_t kEmit>
+// kWaves > 1 (kSmall only): `smem` is this wave's 16 KiB region of a workgroup
+// of kWaves independent waves (lz4_compress_kernel), so the workgroup's
+// barrier is no business of the value loop: LDS ordering within the wave is
+// all it needs (a wave's LDS instructions execute in order).
+template <uint32_t kWaves>
+__device__ __forceinline__ void value_sync() {
+  if constexpr (kWaves == 1) __syncthreads();
+  else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+template <bool kFrame, bool kSmall, uint32_t kEmit, uint32_t kWaves = 1>
 __device__ __forceinline__ void values_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
@@ -1204,9 +1226,13 @@ __device__ __forceinline__ void values_loop(
   uint8_t* s_tab = kSmall ? smem + kT12Lo : smem;
   const uint4 z4 = make_uint4(0, 0, 0, 0);
 
-  using Tab = typename std::conditional<kSmall, Table12, Table16>::type;
+  static_assert(kWaves == 1 || kSmall, "multi-wave workgroups: the Table12 class");
+  using Tab = typename std::conditional<kSmall, Table12T<(kWaves > 1)>, Table16>::type;
   Tab tab;
   if constexpr (!kSmall) tab = Table16(tab16);
+  if constexpr (kSmall && kWaves > 1) tab.base = lds_off(smem);
+  // this wave among the launch's (claims spread over the work queues by it)
+  const uint32_t vb = kWaves > 1 ? blockIdx.x * kWaves + uni(threadIdx.x >> 6) : blockIdx.x;
   if (kSmall) {
     for (uint32_t i = lane; i < kTabBytes / 16u; i += 64u) reinterpret_cast<uint4*>(s_tab)[i] = z4;
   }
@@ -1219,7 +1245,7 @@ __device__ __forceinline__ void values_loop(
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   u32x4 pa[kPrefetch], pb[kPrefetch];
   uint32_t p_head = 0, p_chunks = 0;
-  WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide);
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide, vb, gridDim.x * kWaves);
   uint32_t v = uni(wq.next());
   auto prefetch = [&](uint32_t w) {
     if (w < n) {
@@ -1277,7 +1303,7 @@ __device__ __forceinline__ void values_loop(
       stage_aligned(g, S, s_in);
       for (uint32_t i = lane; i < kTableBytes / 16u; i += 64u) reinterpret_cast<uint4*>(tab16)[i] = z4;
     }
-    __syncthreads();
+    value_sync<kWaves>();
 
     const uint32_t bound = compress_bound(S);
     if (!kFrame) {
@@ -1314,13 +1340,18 @@ __device__ __forceinline__ void values_loop(
 #pragma unroll
       for (uint32_t k = 0; k < kTabBytes / 1024u; ++k) reinterpret_cast<uint4*>(s_tab)[lane + 64u * k] = z4;
     }
-    __syncthreads();
+    value_sync<kWaves>();
     v = vn;
   }
 }
 
-template <bool kFrame, bool kSmall, uint32_t kEmit>
-__global__ __launch_bounds__(64) void lz4_compress_kernel(
+// kWaves (kSmall): waves per workgroup, each compressing its own values in its
+// own 16 KiB region.  LDS is handed out in 1 280-byte steps per workgroup
+// (tools/probe/lds_occupancy, profiles/r05/r05_occ.txt): a one-wave workgroup
+// of 16 KiB takes 13 steps, so 9 fit a CU's 160 KiB; ten waves in one
+// workgroup of exactly 160 KiB hold 10 values per CU.
+template <bool kFrame, bool kSmall, uint32_t kEmit, uint32_t kWaves = 1>
+__global__ __launch_bounds__(64 * kWaves) void lz4_compress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t in_cap,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
@@ -1330,12 +1361,16 @@ __global__ __launch_bounds__(64) void lz4_compress_kernel(
   if (census && census[cls] == 0) return;      // no value of this size class in the batch
   // kSmall: a fixed LDS layout at LDS address 0 (the kernel's only LDS
   // array), so every LDS address is a constant offset (a dynamic
-  // allocation's base costs a v_add per address)
-  constexpr uint32_t kStaticLds = kSmall ? kTable12Bytes + 4096u : 16u;
+  // allocation's base costs a v_add per address); with several waves, wave w's
+  // region at w x 16 KiB
+  constexpr uint32_t kStaticLds = kSmall ? (kTable12Bytes + 4096u) * kWaves : 16u;
+  static_assert(kStaticLds <= 163840u, "gfx950: 160 KiB of LDS per workgroup");
   __shared__ __attribute__((aligned(16))) uint8_t smem_s[kStaticLds];
   extern __shared__ __attribute__((aligned(16))) uint8_t smem_d[];
-  values_loop<kFrame, kSmall, kEmit>(kSmall ? smem_s : smem_d, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
-                              dst_cap, frame_len, ret, work, batch, nq, guide);
+  uint8_t* smem = smem_d;
+  if constexpr (kSmall) smem = kWaves > 1 ? smem_s + (kTable12Bytes + 4096u) * uni(threadIdx.x >> 6) : smem_s;
+  values_loop<kFrame, kSmall, kEmit, kWaves>(smem, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
+                                             dst_cap, frame_len, ret, work, batch, nq, guide);
 }
 
 // ---------------------------------------------------------------------------
@@ -1620,19 +1655,21 @@ __global__ void class_census_kernel(const uint32_t* __restrict__ len, uint32_t n
   }
 }
 
-template <bool F, bool Sm, uint32_t Em>
+template <bool F, bool Sm, uint32_t Em, uint32_t W = 1>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* src_len, uint32_t n, uint32_t min_len, uint32_t in_cap, uint8_t* dst,
                              const uint64_t* dst_off, const uint32_t* dst_cap, uint32_t* frame_len,
                              int32_t* ret, const uint32_t* census = nullptr, uint32_t cls = 0,
                              uint32_t guide = 0) {
-  auto kern = lz4_compress_kernel<F, Sm, Em>;
-  if (lds + (Sm ? kTable12Bytes + kSmallMax : 16u) > kOffLaneLds) return hipErrorInvalidValue;   // see kOffLaneLds
-  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  static_assert(W == 1 || Sm, "multi-wave workgroups: the <= 4 KiB class");
+  auto kern = lz4_compress_kernel<F, Sm, Em, W>;
+  if (W == 1 && lds + (Sm ? kTable12Bytes + kSmallMax : 16u) > kOffLaneLds) return hipErrorInvalidValue;   // see kOffLaneLds
+  if (W > 1 && lds != 0) return hipErrorInvalidValue;   // static LDS only (kOffLaneWG: nothing past 160 KiB)
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n, W);
   uint32_t* work = nullptr;
-  hipError_t e = launch_counter(st, n, grid, &work);
+  hipError_t e = launch_counter(st, n, grid * W, &work);   // (waves >= values: wave b takes value b)
   if (e != hipSuccess) return e;
-  const uint32_t batch = claim_batch(n, grid);
+  const uint32_t batch = claim_batch(n, grid * W);
   // the rocprof (demangled) name
   static const char* const names[2][2][3] = {
       {{"lz4_compress_kernel<false, false, 0u>", "lz4_compress_kernel<false, false, 1u>",
@@ -1643,8 +1680,13 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
         "lz4_compress_kernel<true, false, 2u>"},
        {"lz4_compress_kernel<true, true, 0u>", "lz4_compress_kernel<true, true, 1u>",
         "lz4_compress_kernel<true, true, 2u>"}}};
-  launch_note(names[F][Sm][Em]);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
+  static const char* const names10[2][3] = {
+      {"lz4_compress_kernel<false, true, 0u, 10u>", "lz4_compress_kernel<false, true, 1u, 10u>",
+       "lz4_compress_kernel<false, true, 2u, 10u>"},
+      {"lz4_compress_kernel<true, true, 0u, 10u>", "lz4_compress_kernel<true, true, 1u, 10u>",
+       "lz4_compress_kernel<true, true, 2u, 10u>"}};
+  launch_note(W > 1 ? names10[F][Em] : names[F][Sm][Em]);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap), guide);
   e = hipGetLastError();
   const hipError_t r = work_counter_release(st, work);   // the slot is fenced even when the launch failed
@@ -1777,6 +1819,23 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
       // batched emission when the launch may hold values of kBatchMin bytes
       // and more (a launch of short values only keeps the per-sequence form)
       const bool bat = max_len >= kBatchMin;
+      // ten waves per workgroup (10 values per CU instead of 9, see
+      // lz4_compress_kernel); KDB_LZ4_WG10=0 (tuning builds): one
+#ifndef KDB_LZ4_WG10_DEFAULT
+#define KDB_LZ4_WG10_DEFAULT 1
+#endif
+      static const bool wg10 = kdb_tune("KDB_LZ4_WG10", KDB_LZ4_WG10_DEFAULT) != 0;
+      if (wg10)
+        r = frame ? (bat ? launch_one<true, true, kEmitBatch, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                                                                  dst_off, dst_cap, frame_len, ret, census, 0, guide)
+                         : launch_one<true, true, kEmitDirect, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                                                                   dst_off, dst_cap, frame_len, ret, census, 0, guide))
+                  : (bat ? launch_one<false, true, kEmitBatch, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax,
+                                                                   dst, dst_off, dst_cap, frame_len, ret, census, 0, guide)
+                         : launch_one<false, true, kEmitDirect, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax,
+                                                                    dst, dst_off, dst_cap, frame_len, ret, census, 0,
+                                                                    guide));
+      else
       r = frame ? (bat ? launch_one<true, true, kEmitBatch>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
                                                             dst_off, dst_cap, frame_len, ret, census, 0, guide)
                        : launch_one<true, true, kEmitDirect>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,

@@ -103,10 +103,14 @@ struct WorkQueue {
   // largest value): 1 Mi x 4 KiB compress 9.01 -> 8.85 ms; 100-byte values
   // and the decoders lose more to the extra claims than the tail gives back
   // (profiles/r04_d/r04_y_ab_guided.txt).
-  __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr, uint32_t guide = 0) {
-    if (!c) return WorkQueue{c, n, batch, blockIdx.x, min(blockIdx.x + 1u, n), 1u, 0u, 0u, 0u};
+  // vb / vgrid: this wave's index among the launch's waves and their number
+  // (the workgroup's and the grid's, for one-wave workgroups)
+  __device__ static WorkQueue make(uint32_t* c, uint32_t n, uint32_t batch, uint32_t nr, uint32_t guide = 0,
+                                   uint32_t vb = blockIdx.x, uint32_t vgrid = gridDim.x) {
+    if (!c) return WorkQueue{c, n, batch, vb, min(vb + 1u, n), 1u, 0u, 0u, 0u};
     nr = nr > 1u ? kQueues : 1u;
-    return WorkQueue{c, n, batch, 0u, 0u, nr, (uint32_t)blockIdx.x % nr, nr, guide};
+    // a guided claim divides what is left by guide x (waves per range)
+    return WorkQueue{c, n, batch, 0u, 0u, nr, vb % nr, nr, guide * max(vgrid / nr, 1u)};
   }
   __device__ __forceinline__ void claim() {
     while (left) {
@@ -117,7 +121,7 @@ struct WorkQueue {
         const uint32_t seen = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (seen < hi - lo) {
           if (guide) {
-            const uint32_t per = (hi - lo - seen) / (guide * max(gridDim.x / nr, 1u));
+            const uint32_t per = (hi - lo - seen) / guide;
             b = per < 1u ? 1u : per < batch ? per : batch;
           }
           v = atomicAdd(c, b);
@@ -223,7 +227,7 @@ hipError_t work_counter(hipStream_t st, uint32_t** ctr);
 // after the launches reading a counter slot are queued on st: fences the slot
 // against reuse (launch_util.hip)
 hipError_t work_counter_release(hipStream_t st, uint32_t* ctr);
-uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n);
+uint32_t persistent_grid(const void* kern, size_t lds, uint32_t n, uint32_t waves = 1);
 // service waves (service.h) resident on `dev` right now (kdb_lz4_capi.hip)
 uint32_t services_resident(int dev);
 // The launch's work counter: a direct launch (n no larger than the resident

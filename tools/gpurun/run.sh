@@ -6,6 +6,7 @@
 # Steps (run in the order given, each under its own time limit; the session
 # stops at the first failure and starts nothing more on the GPU):
 #   tests      pytest -m gpu
+#   parity     the codec parity test files only
 #   smoke      __graft_entry__.smoke()
 #   bench      the headline line (bench.py, host-inclusive rate + CPU baseline)
 #   quick      the headline line without the CPU baseline / host-inclusive legs
@@ -58,6 +59,9 @@ for s in "$@"; do
     tests)
       timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu --durations=25 --timeout 300 --timeout-method thread > "${O}_tests.log" 2>&1 || fail tests $? "${O}_tests.log"
       tail -2 "${O}_tests.log" ;;
+    parity)   # the codec parity files only (compress/decompress kernels)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_digests.py tests/test_gpu_fuzz.py tests/test_gpu_batch_emit.py tests/test_gpu_inplace_window.py tests/test_gpu_mixed_ring.py tests/test_gpu_hardening.py -x -v -m gpu --timeout 200 --timeout-method thread > "${O}_parity.log" 2>&1 || fail parity $? "${O}_parity.log"
+      tail -2 "${O}_parity.log" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "${O}_smoke.log" 2>&1 || fail smoke $? "${O}_smoke.log"
       cat "${O}_smoke.log" ;;
