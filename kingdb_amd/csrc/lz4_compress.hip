@@ -194,16 +194,21 @@ constexpr uint32_t kTable12Bytes = 8192u + 4096u;
 constexpr uint32_t kOffLaneLds = 0x10000u;
 
 // byU16 table, 8192 x u16 (values up to 65 546 bytes; positions < 65 536).
-struct Table16 {
+// kWG: the table of one wave of a multi-wave workgroup (its 16 KiB region at
+// `off`): an off lane's index gets bits that put it past the whole 160 KiB
+// (kOffLaneWG) instead of 64 KiB past the table, which would be another
+// wave's region.
+template <bool kWG>
+struct Table16T {
   static constexpr bool kTagged = false;
   uint32_t off;
   struct Slot { uint32_t h; };
-  __device__ Table16(uint16_t* p) : off(lds_off(p)) {}
-  __device__ Table16() : off(0) {}
+  __device__ Table16T(uint16_t* p) : off(lds_off(p)) {}
+  __device__ Table16T() : off(0) {}
   __device__ __forceinline__ uint32_t xchg(uint32_t h, uint32_t p, bool on, Slot& s) const {
     // an off lane addresses past the allocation (see Table12::xchg): mixed
     // batch compress 5.510 -> 5.494 ms (profiles/r04_d/r04_f_ab_exchange_oor16.txt)
-    const uint32_t oor = on ? 0u : 0x8000u;
+    const uint32_t oor = on ? 0u : (kWG ? kOffLaneWG >> 1 : 0x8000u);
     s.h = h | oor;
     const uint32_t sh = (h & 1u) << 4;
     const uint32_t o = mskor_rtn(off + ((s.h & ~1u) << 1), 0xffffu << sh, (p & 0xffffu) << sh);
@@ -213,6 +218,7 @@ struct Table16 {
     ((lds_u16*)(uintptr_t)off)[s.h] = (uint16_t)v;
   }
 };
+using Table16 = Table16T<false>;
 
 // byU32 table (values >= 65547 bytes): 4096 x u32 positions (lz4.cc:383-410).
 struct Table32 {
@@ -1440,6 +1446,11 @@ hipError_t launch_compress_service(hipStream_t st, const SvcBox* ibox, SvcBox* o
 static_assert(kTable12Bytes + kSmallMax <= kOffLaneLds, "Table12 kernels: off lanes must address past the LDS");
 static_assert(kTableBytes + kMidLdsMax <= kOffLaneLds, "the LDS-staged class: off lanes must address past the LDS");
 static_assert(4096u * 4u <= kOffLaneLds, "Table32 kernels: off lanes must address past the LDS");
+// the compact byU32 kernel: Table24T's off lanes address its byte plane at
+// off + 8192 + (h | 0x8000), 40 KiB past the table's base, and the ring
+// follows the table: everything must stay below that
+static_assert(Table24T::kBytes + RingSrcC::kR + RingSrcC::kMirror <= 8192u + 0x8000u,
+              "Table24T kernels: off lanes must address past the LDS");
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
   // 16 KiB: 10 per CU
@@ -1455,7 +1466,7 @@ size_t compress_lds_bytes(uint32_t max_len) {
 // value.  Waves claim up to 16 values at a time and compress the ones of this class.
 // kCompact (byU32 launches whose values are all at most kTagMaxLen bytes):
 // Table24T and the 2 KiB ring in 14.1 KiB of LDS (10 waves per CU).
-template <bool kFrame, bool kWide, bool kCompact = false>
+template <bool kFrame, bool kWide, bool kCompact = false, uint32_t kWaves = 1>
 __device__ __forceinline__ void big_values(
     uint32_t* const tab32, uint8_t* const ring, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t min_len, uint32_t max_len,
@@ -1463,10 +1474,11 @@ __device__ __forceinline__ void big_values(
     uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch) {
   const uint32_t lane = lane_id();
   // byU32 (kWide): 4096 x u32; byU16: the same 16 KiB as 8192 x u16
-  using Tab = typename std::conditional<kWide, Table32, Table16>::type;
+  static_assert(kWaves == 1 || !kWide, "multi-wave workgroups: the byU16 table");
+  using Tab = typename std::conditional<kWide, Table32, Table16T<(kWaves > 1)>>::type;
   Tab tab;
   if constexpr (kWide) tab = Table32(tab32);
-  else tab = Table16(reinterpret_cast<uint16_t*>(tab32));
+  else tab = Tab(reinterpret_cast<uint16_t*>(tab32));
   const Table32T tabt(tab32);
   const Table24T tabc(tab32);
   static_assert(!kCompact || kWide, "the compact table is byU32's");
@@ -1475,9 +1487,9 @@ __device__ __forceinline__ void big_values(
 #pragma unroll 1
   for (;;) {
     uint32_t c0 = 0;
-    if (!work) {                                 // direct launch: value blockIdx.x, once
+    if (!work) {                                 // direct launch: value <this wave's index>, once
       if (direct_done) break;
-      c0 = blockIdx.x;
+      c0 = kWaves > 1 ? blockIdx.x * kWaves + uni(threadIdx.x >> 6) : blockIdx.x;
       direct_done = true;
     } else {
       if (lane == 0) c0 = atomicAdd(work, batch);
@@ -1608,23 +1620,29 @@ __global__ __launch_bounds__(64) void lz4_compress_big_compact_kernel(
 // small class fills the in-place tail instead of competing with its start
 // (two concurrent launches split the CUs from the start and left the
 // in-place values' last rounds alone on the GPU).
-template <bool kFrame>
-__global__ __launch_bounds__(64) void lz4_compress_mixed_kernel(
+// kWaves: waves per workgroup, each in its own 16 KiB region (10 per CU
+// instead of 9, as lz4_compress_kernel).
+template <bool kFrame, uint32_t kWaves = 1>
+__global__ __launch_bounds__(64 * kWaves) void lz4_compress_mixed_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ src_len, uint32_t n, uint32_t big_min, uint32_t big_max,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off, const uint32_t* __restrict__ dst_cap,
     uint32_t* __restrict__ frame_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work_big,
     uint32_t batch_big, uint32_t* __restrict__ work_small, uint32_t batch_small, uint32_t nq) {
-  __shared__ __attribute__((aligned(16))) uint32_t smem32[(kTable12Bytes + kSmallMax) / 4u];
-  big_values<kFrame, false>(smem32, nullptr, src, src_off, src_len, n, big_min, big_max, dst, dst_off, dst_cap, frame_len,
-                            ret, work_big, batch_big);
-  __syncthreads();
+  constexpr uint32_t kRegion = kTable12Bytes + kSmallMax;
+  static_assert(kRegion * kWaves <= 163840u, "gfx950: 160 KiB of LDS per workgroup");
+  __shared__ __attribute__((aligned(16))) uint32_t smem32_all[kRegion * kWaves / 4u];
+  uint32_t* smem32 = kWaves > 1 ? smem32_all + kRegion / 4u * uni(threadIdx.x >> 6) : smem32_all;
+  big_values<kFrame, false, false, kWaves>(smem32, nullptr, src, src_off, src_len, n, big_min, big_max, dst, dst_off,
+                                           dst_cap, frame_len, ret, work_big, batch_big);
+  value_sync<kWaves>();
 #ifndef KDB_LZ4_MIXED_EMIT
 #define KDB_LZ4_MIXED_EMIT kEmitPerValue
 #endif
   // the small pass: 100-byte and 4 KiB values together, each its own form
-  values_loop<kFrame, true, KDB_LZ4_MIXED_EMIT>(reinterpret_cast<uint8_t*>(smem32), src, src_off, src_len, n, 0u, kSmallMax, dst,
-                            dst_off, dst_cap, frame_len, ret, work_small, batch_small, nq, 0u);
+  values_loop<kFrame, true, KDB_LZ4_MIXED_EMIT, kWaves>(reinterpret_cast<uint8_t*>(smem32), src, src_off, src_len, n, 0u,
+                                                        kSmallMax, dst, dst_off, dst_cap, frame_len, ret, work_small,
+                                                        batch_small, nq, 0u);
 }
 
 // Values per size class (len <= b0, <= b1, <= b2, above), so that a class
@@ -1663,7 +1681,12 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
                              uint32_t guide = 0) {
   static_assert(W == 1 || Sm, "multi-wave workgroups: the <= 4 KiB class");
   auto kern = lz4_compress_kernel<F, Sm, Em, W>;
-  if (W == 1 && lds + (Sm ? kTable12Bytes + kSmallMax : 16u) > kOffLaneLds) return hipErrorInvalidValue;   // see kOffLaneLds
+  // see kOffLaneLds: the off lanes' first address (Table12 at kT12Lo in the
+  // static 16 KiB; Table16 at the dynamic allocation, after the 16 static
+  // bytes) must lie past the whole allocation
+  const size_t alloc = (Sm ? kTable12Bytes + kSmallMax : 16u) + lds;
+  const size_t off_lane = Sm ? kOffLaneLds + kT12Lo : 16u + kOffLaneLds;
+  if (W == 1 && alloc > off_lane) return hipErrorInvalidValue;
   if (W > 1 && lds != 0) return hipErrorInvalidValue;   // static LDS only (kOffLaneWG: nothing past 160 KiB)
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n, W);
   uint32_t* work = nullptr;
@@ -1672,14 +1695,14 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   const uint32_t batch = claim_batch(n, grid * W);
   // the rocprof (demangled) name
   static const char* const names[2][2][3] = {
-      {{"lz4_compress_kernel<false, false, 0u>", "lz4_compress_kernel<false, false, 1u>",
-        "lz4_compress_kernel<false, false, 2u>"},
-       {"lz4_compress_kernel<false, true, 0u>", "lz4_compress_kernel<false, true, 1u>",
-        "lz4_compress_kernel<false, true, 2u>"}},
-      {{"lz4_compress_kernel<true, false, 0u>", "lz4_compress_kernel<true, false, 1u>",
-        "lz4_compress_kernel<true, false, 2u>"},
-       {"lz4_compress_kernel<true, true, 0u>", "lz4_compress_kernel<true, true, 1u>",
-        "lz4_compress_kernel<true, true, 2u>"}}};
+      {{"lz4_compress_kernel<false, false, 0u, 1u>", "lz4_compress_kernel<false, false, 1u, 1u>",
+        "lz4_compress_kernel<false, false, 2u, 1u>"},
+       {"lz4_compress_kernel<false, true, 0u, 1u>", "lz4_compress_kernel<false, true, 1u, 1u>",
+        "lz4_compress_kernel<false, true, 2u, 1u>"}},
+      {{"lz4_compress_kernel<true, false, 0u, 1u>", "lz4_compress_kernel<true, false, 1u, 1u>",
+        "lz4_compress_kernel<true, false, 2u, 1u>"},
+       {"lz4_compress_kernel<true, true, 0u, 1u>", "lz4_compress_kernel<true, true, 1u, 1u>",
+        "lz4_compress_kernel<true, true, 2u, 1u>"}}};
   static const char* const names10[2][3] = {
       {"lz4_compress_kernel<false, true, 0u, 10u>", "lz4_compress_kernel<false, true, 1u, 10u>",
        "lz4_compress_kernel<false, true, 2u, 10u>"},
@@ -1718,19 +1741,25 @@ static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t*
   return e != hipSuccess ? e : r;
 }
 
+#ifndef KDB_LZ4_MIXED_WAVES
+#define KDB_LZ4_MIXED_WAVES 10
+#endif
 template <bool F>
 static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                                uint32_t n, uint32_t big_min, uint32_t big_max, uint8_t* dst, const uint64_t* dst_off,
                                const uint32_t* dst_cap, uint32_t* frame_len, int32_t* ret) {
-  auto kern = lz4_compress_mixed_kernel<F>;
-  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n);
+  constexpr uint32_t W = KDB_LZ4_MIXED_WAVES;
+  auto kern = lz4_compress_mixed_kernel<F, W>;
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), 0, n, W);
   uint32_t *wb = nullptr, *ws = nullptr;
-  hipError_t e = launch_counter(st, n, grid, &wb);
-  if (e == hipSuccess) e = launch_counter(st, n, grid, &ws);
+  hipError_t e = launch_counter(st, n, grid * W, &wb);
+  if (e == hipSuccess) e = launch_counter(st, n, grid * W, &ws);
   if (e == hipSuccess) {
-    const uint32_t bb = wb ? claim_batch(n, grid) : 1u, bs = claim_batch(n, grid);
-    launch_note(F ? "lz4_compress_mixed_kernel<true>" : "lz4_compress_mixed_kernel<false>");
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, src, src_off, src_len, n, big_min, big_max, dst, dst_off,
+    const uint32_t bb = wb ? claim_batch(n, grid * W) : 1u, bs = claim_batch(n, grid * W);
+    static_assert(W == 1 || W == 10, "the rocprof names below");
+    launch_note(W > 1 ? (F ? "lz4_compress_mixed_kernel<true, 10u>" : "lz4_compress_mixed_kernel<false, 10u>")
+                      : (F ? "lz4_compress_mixed_kernel<true, 1u>" : "lz4_compress_mixed_kernel<false, 1u>"));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), 0, st, src, src_off, src_len, n, big_min, big_max, dst, dst_off,
                        dst_cap, frame_len, ret, wb, bb, ws, bs, work_queues(kSmallMax));
     e = hipGetLastError();
   }

@@ -366,6 +366,14 @@ __device__ __forceinline__ void prefetch_value(uint4& p0, uint4& p1, uint4& p2, 
   }
 }
 
+// Between a value's LDS staging and its decode, and between values: the
+// wave's own LDS instructions execute in order, so a workgroup of several
+// independent waves needs no barrier (a one-wave workgroup keeps the one it had).
+__device__ __forceinline__ void value_sync(uint32_t waves) {
+  if (waves > 1) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  else __syncthreads();
+}
+
 template <bool kFrame, uint32_t kPF>
 __device__ __forceinline__ void small_decode_loop(
     uint8_t* const smem, const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
@@ -373,11 +381,13 @@ __device__ __forceinline__ void small_decode_loop(
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t skip_big, uint32_t nq, uint32_t guide = 0) {
+    uint32_t skip_big, uint32_t nq, uint32_t guide = 0, uint32_t waves = 1) {
   const uint32_t lane = lane_id();
   // [staged block + 16 zero bytes][output window + 64 bytes of slack for the
   // decoder's unmasked 64-byte steps]; the register window may read 256 bytes
-  // past the block, into the output window (decompress_lds_bytes)
+  // past the block, into the output window (decompress_lds_bytes).  With
+  // `waves` > 1 (lz4_decompress_kernel) `smem` is this wave's region of the
+  // workgroup's LDS and the waves never wait for one another.
   uint8_t* s_in = smem;
   const uint32_t s_in_cap = (in_cap + 32u + 15u) & ~15u;
   uint8_t* s_out = smem + s_in_cap;
@@ -386,7 +396,8 @@ __device__ __forceinline__ void small_decode_loop(
   uint4 pf0 = {}, pf1 = {}, pf2 = {}, pf3 = {}, pf4 = {};
   uint32_t pf_head = 0, pf_chunks = 0;
 
-  WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide);
+  const uint32_t vb = waves > 1 ? blockIdx.x * waves + uni(threadIdx.x >> 6) : blockIdx.x;
+  WorkQueue wq = WorkQueue::make(work, n, batch, nq, guide, vb, gridDim.x * waves);
   uint32_t v = uni(wq.next());
   prefetch_value<kPF>(pf0, pf1, pf2, pf3, pf4, pf_head, pf_chunks, v, n, src, src_off, in_len, s_in_cap);
 #pragma unroll 1
@@ -458,7 +469,7 @@ __device__ __forceinline__ void small_decode_loop(
       }
       const uint32_t head = st_chunks ? st_head + (kFrame ? 8u : 0u) : stage_to_lds(g, (uint32_t)csize, s_in);
       if (lane < 16u) s_in[head + (uint32_t)csize + lane] = 0;   // OOB bytes read as 0
-      __syncthreads();
+      value_sync(waves);
       const int r = decode_block(s_in, head, csize, s_out, osize, tgt);
       if (r > 0) flush_lds_to_global(o, s_out, 0, (uint32_t)r);
       if (lane == 0) {
@@ -471,22 +482,27 @@ __device__ __forceinline__ void small_decode_loop(
         }
       }
     } while (false);
-    __syncthreads();
+    value_sync(waves);
     v = vn;
   }
 }
 
+// Workgroups of blockDim.x / 64 independent waves, each with its own `region`
+// bytes of the dynamic LDS (launch_one picks the count: LDS is handed out in
+// 1 280-byte steps per workgroup, so one-wave workgroups of the headline's
+// 7 264 bytes held 21 waves per CU, two of eleven hold 22).
 template <bool kFrame, uint32_t kPF>
-__global__ __launch_bounds__(64) void lz4_decompress_kernel(
+__global__ __launch_bounds__(1024) void lz4_decompress_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const uint32_t* __restrict__ in_len, uint32_t n, uint32_t in_cap, uint32_t out_cap_max,
     uint8_t* __restrict__ dst, const uint64_t* __restrict__ dst_off,
     const uint32_t* __restrict__ out_cap, const uint32_t* __restrict__ target,
     uint32_t* __restrict__ out_len, int32_t* __restrict__ ret, uint32_t* __restrict__ work, uint32_t batch,
-    uint32_t skip_big, uint32_t nq, uint32_t guide) {
+    uint32_t skip_big, uint32_t nq, uint32_t guide, uint32_t region) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  small_decode_loop<kFrame, kPF>(smem, src, src_off, in_len, n, in_cap, out_cap_max, dst, dst_off, out_cap, target,
-                            out_len, ret, work, batch, skip_big, nq, guide);
+  const uint32_t waves = blockDim.x >> 6;
+  small_decode_loop<kFrame, kPF>(smem + region * uni(threadIdx.x >> 6), src, src_off, in_len, n, in_cap, out_cap_max,
+                                 dst, dst_off, out_cap, target, out_len, ret, work, batch, skip_big, nq, guide, waves);
 }
 
 // ---------------------------------------------------------------------------
@@ -1014,6 +1030,31 @@ size_t decompress_lds_bytes(uint32_t max_in, uint32_t max_out) {
   return in_bytes + (out_bytes > 272u ? out_bytes : 272u);
 }
 
+// Waves per workgroup for the LDS decoder with `region` bytes per wave: the
+// count that puts the most waves on a CU, by the measured allocation rule
+// (LDS in 1 280-byte steps per workgroup out of 160 KiB; tools/probe/
+// lds_occupancy, profiles/r05/r05_occ.txt) and capped by what the kernel's
+// registers allow (the occupancy API for one-wave workgroups without LDS).
+// KDB_LZ4_DWAVES (tuning builds) forces a count.
+static uint32_t decode_waves(const void* kern, size_t region) {
+  static const uint32_t forced = (uint32_t)kdb_tune("KDB_LZ4_DWAVES", 0);
+  if (forced) return forced > 16u ? 16u : forced;
+  int regs = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&regs, kern, 64, 0) != hipSuccess || regs < 1) return 1;
+  constexpr size_t kStep = 1280, kLds = 163840;
+  uint32_t best = 1, best_waves = 0;
+  for (uint32_t w = 1; w <= 16; ++w) {
+    const size_t need = (region * w + kStep - 1) / kStep * kStep;
+    if (need > kLds) break;
+    const uint32_t waves = std::min<uint32_t>((uint32_t)(kLds / need) * w, (uint32_t)regs);
+    if (waves > best_waves) {
+      best = w;
+      best_waves = waves;
+    }
+  }
+  return best;
+}
+
 template <bool F>
 static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, const uint64_t* src_off,
                              const uint32_t* in_len, uint32_t n, uint32_t max_in, uint32_t max_out, uint8_t* dst,
@@ -1023,16 +1064,17 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   // launch fits them (8 fewer VGPRs: 6 waves per SIMD instead of 5)
   const bool pf3 = max_in <= 3057u;
   auto kern = pf3 ? lz4_decompress_kernel<F, 3u> : lz4_decompress_kernel<F, 5u>;
-  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
+  const uint32_t W = decode_waves(reinterpret_cast<const void*>(kern), lds);
+  const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds * W, n, W);
   uint32_t* work = nullptr;
-  hipError_t e = launch_counter(st, n, grid, &work);
+  hipError_t e = launch_counter(st, n, grid * W, &work);   // (waves >= values: wave b takes value b)
   if (e != hipSuccess) return e;
-  const uint32_t batch = claim_batch(n, grid);
+  const uint32_t batch = claim_batch(n, grid * W);
   launch_note(F ? (pf3 ? "lz4_decompress_kernel<true, 3u>" : "lz4_decompress_kernel<true, 5u>")
                 : (pf3 ? "lz4_decompress_kernel<false, 3u>" : "lz4_decompress_kernel<false, 5u>"));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, src, src_off, in_len, n, max_in, max_out, dst, dst_off,
-                     out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out),
-                     decode_guide(max_out));
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), lds * W, st, src, src_off, in_len, n, max_in, max_out, dst,
+                     dst_off, out_cap, target, out_len, ret, work, batch, skip_big, work_queues(max_out),
+                     decode_guide(max_out), (uint32_t)lds);
   e = hipGetLastError();
   const hipError_t r = work_counter_release(st, work);   // the slot is fenced even when the launch failed
   return e != hipSuccess ? e : r;

@@ -90,6 +90,12 @@ class HostPipeline:
         # 19.7 GiB/s round trip; 1 and 1: 17.4)
         self.dstreams = [Stream() for _ in range(max(1, nstreams, cdrain, ddrain))]
         self.cdrain, self.ddrain = max(1, cdrain), max(1, ddrain)
+        self.dserial = False
+        self.cserial = False
+        # serial modes: one stream per copy direction and phase, never used for
+        # anything else (a copy stream reused for the other direction measured
+        # slow: tools/hostpipe_probe.py)
+        self.dup, self.ddown, self.cup = Stream(), Stream(), Stream()
         # host side (pinned): raw values, packed frames, decoded values, metadata
         self.h_raw = PinnedBuffer(n * size)
         self.h_frames = PinnedBuffer(n * self.slot)
@@ -159,18 +165,24 @@ class HostPipeline:
             chunk_off[c] = host_off
             host_off += tot
 
+        serial = self.cserial
+        hdone = [Event() for _ in range(self.nchunks)] if serial else None
         t0 = time.perf_counter()
         for c in range(self.nchunks):
             lo, hi = self._range(c)
             m = hi - lo
             st = self.streams[c % S].ptr
             cm, dm = self.h_cmeta.ptr, self.d_cmeta.ptr
-            e0 = self._mark(self.streams[c % S])
+            hs = self.cup if serial else self.streams[c % S]   # the stream of the chunk's host-to-device copies
+            e0 = self._mark(hs)
             for base, w in ((0, 8), (8 * n, 4), (12 * n, 8)):
-                _lib.check(L.kdb_lz4_memcpy_h2d(dm + base + w * lo, cm + base + w * lo, w * m, st), "h2d meta")
-            _lib.check(L.kdb_lz4_memcpy_h2d(self.d_raw.ptr + lo * size, self.h_raw.ptr + lo * size, m * size, st),
+                _lib.check(L.kdb_lz4_memcpy_h2d(dm + base + w * lo, cm + base + w * lo, w * m, hs.ptr), "h2d meta")
+            _lib.check(L.kdb_lz4_memcpy_h2d(self.d_raw.ptr + lo * size, self.h_raw.ptr + lo * size, m * size, hs.ptr),
                        "h2d raw")
-            self._span("h2d", c, e0, self.streams[c % S])
+            self._span("h2d", c, e0, hs)
+            if serial:
+                hdone[c].record(self.cup)
+                _lib.check(L.kdb_lz4_stream_wait_event(st, hdone[c].ptr), "stream_wait_event")
             e0 = self._mark(self.streams[c % S])
             flen = self.d_cres.ptr + 4 * lo
             stat = self.d_cres.ptr + 4 * n + 4 * lo
@@ -192,7 +204,7 @@ class HostPipeline:
                 drain(c - (S - 1))
         for c in range(max(0, self.nchunks - (S - 1)), self.nchunks):
             drain(c)
-        for s in self.streams + self.dstreams:
+        for s in self.streams + self.dstreams + [self.cup]:
             s.sync()
         t = time.perf_counter() - t0
         self.frame_bytes = host_off
@@ -210,8 +222,18 @@ class HostPipeline:
     def frames(self) -> bytes:
         return self.h_frames.np[: self.frame_bytes].tobytes()
 
-    def decompress(self) -> float:
-        """Packed host frames (as produced by compress()) -> host raw values."""
+    def decompress(self, serial: bool | None = None) -> float:
+        """Packed host frames (as produced by compress()) -> host raw values.
+
+        serial (default: self.dserial): every chunk's host-to-device copies on
+        one stream, in chunk order, and every device-to-host copy on another,
+        each chunk's decode on a compute stream between them (events): the two
+        directions then stream side by side, each in order, instead of 4 + 4
+        copy queues contending in each direction."""
+        if serial is None:
+            serial = self.dserial
+        if serial:
+            return self._decompress_serial()
         L = lib()
         n, size = self.n, self.size
         S = len(self.streams)
@@ -254,6 +276,50 @@ class HostPipeline:
             s.sync()
         return time.perf_counter() - t0
 
+    def _decompress_serial(self) -> float:
+        L = lib()
+        n, size = self.n, self.size
+        S = len(self.streams)
+        dm = self.h_dmeta.np
+        dm[: 8 * n] = self.frame_off[:n].view(np.uint8)
+        dm[8 * n: 12 * n] = np.diff(self.frame_off).astype(np.uint32).view(np.uint8)
+        max_in = int(np.diff(self.frame_off).max()) if n else 0
+        up, down = self.dup, self.ddown
+        hdone = [Event() for _ in range(self.nchunks)]
+        kdone = [Event() for _ in range(self.nchunks)]
+        t0 = time.perf_counter()
+        for c in range(self.nchunks):
+            lo, hi = self._range(c)
+            m = hi - lo
+            f0, f1 = int(self.frame_off[lo]), int(self.frame_off[hi])
+            e0 = self._mark(up)
+            _lib.check(L.kdb_lz4_memcpy_h2d(self.d_packed.ptr + f0, self.h_frames.ptr + f0, f1 - f0, up.ptr), "h2d frames")
+            for base, w in ((0, 8), (8 * n, 4)):
+                _lib.check(L.kdb_lz4_memcpy_h2d(self.d_dmeta.ptr + base + w * lo, self.h_dmeta.ptr + base + w * lo,
+                                                w * m, up.ptr), "h2d meta")
+            self._span("h2d", c, e0, up)
+            hdone[c].record(up)
+            ks = self.streams[c % S]
+            _lib.check(L.kdb_lz4_stream_wait_event(ks.ptr, hdone[c].ptr), "stream_wait_event")
+            e0 = self._mark(ks)
+            _lib.check(L.kdb_lz4_decompress_frames_batch(
+                ks.ptr, self.d_packed.ptr, self.d_dmeta.ptr + 8 * lo, self.d_dmeta.ptr + 8 * n + 4 * lo, m, max_in,
+                size, self.d_out.ptr, self.d_dconst.ptr + 8 * lo, self.d_dconst.ptr + 8 * n + 4 * lo,
+                self.d_dres.ptr + 4 * lo, self.d_dres.ptr + 4 * n + 4 * lo), "decompress_frames_batch")
+            self._span("kernel", c, e0, ks)
+            kdone[c].record(ks)
+            _lib.check(L.kdb_lz4_stream_wait_event(down.ptr, kdone[c].ptr), "stream_wait_event")
+            e0 = self._mark(down)
+            _lib.check(L.kdb_lz4_memcpy_d2h(self.h_out.ptr + lo * size, self.d_out.ptr + lo * size, m * size,
+                                            down.ptr), "d2h out")
+            self._span("d2h", c, e0, down)
+            for base in (4 * lo, 4 * n + 4 * lo):
+                _lib.check(L.kdb_lz4_memcpy_d2h(self.h_dres.ptr + base, self.d_dres.ptr + base, 4 * m, down.ptr),
+                           "d2h results")
+        for s in self.streams + self.dstreams + [self.dup, self.ddown]:
+            s.sync()
+        return time.perf_counter() - t0
+
     def _copies(self, h2d: bool, d2h: bool) -> float:
         """The link alone: n*size bytes in the pipeline's chunks over its
         streams, one or both directions at once.  Wall seconds."""
@@ -290,7 +356,7 @@ class HostPipeline:
             self._trace = []
             base = Event()
             base.record(self.streams[0])
-            for ds in self.dstreams:          # every traced stream starts after the base event
+            for ds in self.dstreams + [self.dup, self.ddown, self.cup]:   # every traced stream starts after the base event
                 _lib.check(lib().kdb_lz4_stream_wait_event(ds.ptr, base.ptr), "stream_wait_event")
             wall = getattr(self, phase)()
             spans, self._trace = self._trace, None

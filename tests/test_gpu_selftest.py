@@ -61,13 +61,13 @@ def test_last_kernels_names(gpu):
     return at once): the names are rocprof's."""
     import kingdb_amd as K
     K.compress_frames([b"x" * 4096] * 4)
-    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u>"]   # batched emission
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u, 10u>"]   # batched emission
     K.compress_frames([b"x" * 100] * 4)
-    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 0u>"]   # short values: per sequence
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 0u, 10u>"]   # short values: per sequence
     K.compress_frames([b"x" * 6000] * 4)
-    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u>", "lz4_compress_kernel<true, false, 1u>"]
+    assert K.last_kernels() == ["lz4_compress_kernel<true, true, 1u, 10u>", "lz4_compress_kernel<true, false, 1u, 1u>"]
     K.compress_frames([b"x" * 4096, b"y" * 20000])
-    assert K.last_kernels() == ["lz4_compress_mixed_kernel<true>", "lz4_compress_kernel<true, false, 1u>"]
+    assert K.last_kernels() == ["lz4_compress_mixed_kernel<true, 10u>", "lz4_compress_kernel<true, false, 1u, 1u>"]
     K.compress_frames([b"x" * 100000])                  # byU32, every value <= 1 MiB: the compact table
     assert "lz4_compress_big_compact_kernel<true>" in K.last_kernels()
     K.compress_frames([b"x" * 100000, b"z" * ((1 << 20) + 1)])
