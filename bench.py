@@ -252,10 +252,15 @@ def host_inclusive(batch, n: int, size: int, args) -> dict:
         "pcie_bytes": {"compress_h2d": int(raw) + 20 * n, "compress_d2h": hp.frame_bytes + 8 * n,
                        "decompress_h2d": hp.frame_bytes + 12 * n, "decompress_d2h": int(raw) + 8 * n},
         "chunk": hp.chunk, "streams": len(hp.streams),
+        "copies": ("serial: each phase's H2D copies in chunk order on one stream, D2H on another, no copy stream "
+                   "used for both directions" if hp.cserial and hp.dserial else "per-chunk streams"),
         "timing": "host wall clock, first enqueue to last byte in pinned host memory; median of 3 after 1 warm-up",
     }
     # where the wall time goes (traced runs after the timed ones; weak #9 of round 2)
     res["stall_profile"] = hp.profile()
+    # the traced runs measure the same pipeline: their wall time against the timed median
+    res["traced_over_timed"] = {ph: round(res["stall_profile"][ph]["wall_ms"] / res[ph + "_ms"], 3)
+                                for ph in ("compress", "decompress")}
     hp.free()
     return res
 

@@ -90,11 +90,18 @@ class HostPipeline:
         # 19.7 GiB/s round trip; 1 and 1: 17.4)
         self.dstreams = [Stream() for _ in range(max(1, nstreams, cdrain, ddrain))]
         self.cdrain, self.ddrain = max(1, cdrain), max(1, ddrain)
-        self.dserial = False
-        self.cserial = False
-        # serial modes: one stream per copy direction and phase, never used for
-        # anything else (a copy stream reused for the other direction measured
-        # slow: tools/hostpipe_probe.py)
+        # Serial copies (round 6, the default): each phase's host-to-device
+        # copies in chunk order on a stream of their own, the decode's
+        # device-to-host copies likewise, and no copy stream ever carries the
+        # other direction.  Measured on MI355X (tools/hostpipe_probe.py,
+        # profiles/r06/r06_e_hostprobe.json): compress 99-110 -> 88.6 ms,
+        # decompress 108-121 -> 85.8 ms (its floor is 4.3 GB of D2H at
+        # 57 GB/s, ~75 ms).  The per-chunk streams of round 3 left the 4 + 4
+        # copy queues of each direction contending, and a decompress that
+        # reused streams the compress had copied the other way on ran at
+        # 124 ms.
+        self.dserial = True
+        self.cserial = True
         self.dup, self.ddown, self.cup = Stream(), Stream(), Stream()
         # host side (pinned): raw values, packed frames, decoded values, metadata
         self.h_raw = PinnedBuffer(n * size)
@@ -352,6 +359,11 @@ class HostPipeline:
             t = min(self._copies(h, d) for _ in range(3))
             link[name + "_gbs"] = round((raw * (h + d)) / t / 1e9, 2)
         out = {"link_alone": link}
+        # one untraced round trip first: the first compress after other copy
+        # traffic runs ~10 % slow (profiles/r06/r06_e_hostprobe.json), and the
+        # traced runs are to show the pipeline the timed runs measure
+        self.compress()
+        self.decompress()
         for phase in ("compress", "decompress"):
             self._trace = []
             base = Event()
