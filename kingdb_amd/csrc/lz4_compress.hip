@@ -8,7 +8,8 @@
 // Persistent launch: one wavefront (workgroup of 64) per resident slot takes
 // values from device-scope work counters, one value ahead.  Size classes
 // (launch_compress): values <= 4 KiB are staged in LDS next to a two-plane
-// 12-bit table (16 KiB per value, 10 values per CU) and the next value is
+// 12-bit table (16 KiB per value; ten such waves per 160 KiB workgroup, so 10
+// values per CU -- one-wave workgroups of 16 KiB held 9) and the next value is
 // prefetched into registers while the current one is parsed; 4-8 KiB values
 // are staged next to a u16 table; larger values are read in place from
 // HBM/L2 with only the table (u16 for byU16, u32 for byU32) in LDS.  The
@@ -110,7 +111,9 @@ __device__ __forceinline__ void mskor(uint32_t a, uint32_t m, uint32_t d) {
 // byU16 table for values <= 4 KiB, whose positions fit 12 bits: two planes,
 // the low bytes (8192 x u8) and the high nibbles (4096 x u8, two per byte),
 // 12 KiB instead of 16 -- 16 KiB of LDS per value with its bytes, so 10
-// values per CU (the parse is latency-bound: occupancy is speed).  Cleared per
+// values per CU in ten-wave workgroups of 160 KiB (the hardware allocates LDS
+// per workgroup in 1 280-byte steps: one-wave workgroups of 16 KiB hold 9;
+// the parse is latency-bound: occupancy is speed).  Cleared per
 // value (12 x 16 B stores per lane).  The layout is fixed (the kernels that
 // use it have one static LDS array, at LDS address 0): the value at [0, 4096),
 // the low bytes at kT12Lo, the high nibbles at kT12Hi -- both planes are
@@ -1453,7 +1456,7 @@ static_assert(Table24T::kBytes + RingSrcC::kR + RingSrcC::kMirror <= 8192u + 0x8
               "Table24T kernels: off lanes must address past the LDS");
 // LDS bytes a launch needs for values up to max_len bytes.
 size_t compress_lds_bytes(uint32_t max_len) {
-  // 16 KiB: 10 per CU
+  // 16 KiB: 10 per CU in ten-wave workgroups
   if (max_len <= kSmallMax) return kTable12Bytes + kSmallMax;
   return kTableBytes + (((size_t)max_len + 15u) & ~(size_t)15u);
 }
@@ -1877,7 +1880,8 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
     }
     // 4 KiB .. 8 KiB: the value staged in LDS (24 KiB with the table: 6 per CU);
     // 8 KiB .. 65 546 B: read in place from HBM/L2 with only the table in LDS
-    // (10 per CU) -- measured faster than 2-5 LDS-staged values per CU.
+    // (10 per CU by hipOccupancy, 9 by the 1 280-byte LDS steps) -- measured
+    // faster than 2-5 LDS-staged values per CU.
     if (on[1]) {
       const uint32_t top = max_len < hi[1] ? max_len : hi[1];   // (host min() is signed)
       const size_t lds = compress_lds_bytes(top);

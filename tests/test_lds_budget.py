@@ -74,8 +74,11 @@ def test_multiwave_workgroups():
     """Several independent waves per workgroup pay the 1 280-byte step once per
     workgroup: ten 16 KiB compress waves fill exactly 160 KiB (10 per CU
     where one-wave workgroups hold 9), and the headline decoder's 7 264-byte
-    waves go two workgroups of eleven (22 per CU where one-wave ones hold 21)."""
+    waves (2 308-byte largest frame + the 4 KiB window: 6 512 bytes) go eight
+    workgroups of three (24 per CU, the register limit, where one-wave ones
+    hold 21)."""
     assert groups_per_cu(16384) * 1 == 9 and groups_per_cu(16384 * 10) * 10 == 10
+    assert groups_per_cu(6512) == 21 and decode_waves(6512, 24) == (3, 24)
     assert decode_waves(7264, 24) == (11, 22)
     assert decode_waves(6400, 24) == (1, 24)        # one-wave workgroups already at the register cap
     assert decode_waves(8704, 24) == (1, 18)        # the mixed decoder's ring region: nothing to gain
