@@ -134,11 +134,15 @@ class HostPipeline:
         self.frame_bytes = 0
         self.frame_off = np.zeros(n + 1, np.uint64)
         self._trace = None        # [(kind, chunk, start Event, end Event)] while profile() runs
+        self._pool = []           # events for the traced runs, made before them
 
     def _mark(self, st) -> "Event | None":
         if self._trace is None:
             return None
-        e = Event()
+        # from a pool made before the traced run: creating events inside it
+        # delayed the compress loop's enqueues behind its host waits (traced
+        # compress 114 ms against 90 timed, profiles/r06/r06_g_bench.json)
+        e = self._pool.pop() if self._pool else Event()
         e.record(st)
         return e
 
@@ -365,6 +369,7 @@ class HostPipeline:
         self.compress()
         self.decompress()
         for phase in ("compress", "decompress"):
+            self._pool = [Event() for _ in range(8 * self.nchunks + 8)]
             self._trace = []
             base = Event()
             base.record(self.streams[0])
