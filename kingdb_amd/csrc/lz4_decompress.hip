@@ -526,72 +526,16 @@ constexpr uint32_t kIMirror = 512u;
 template <uint32_t kORing, uint32_t kIR>
 constexpr size_t ring_lds() { return kORing + kIR + kIMirror; }
 
-// kAhead (the 1 MiB parts' 8 KiB ring, KDB_LZ4_IRING_AHEAD): each refill also
-// issues the loads of the NEXT half into registers, which land while that
-// half's bytes are decoded, so a refill waits for nothing but its stores'
-// acknowledgements instead of a fresh HBM round trip.  32 more VGPRs: only
-// where the batch's parts, not the registers, bound the waves in flight.
-#ifndef KDB_LZ4_IRING_AHEAD
-#define KDB_LZ4_IRING_AHEAD 1
-#endif
-template <uint32_t kIR, bool kAhead = false>
+template <uint32_t kIR>
 struct InRing {
   static constexpr uint32_t kIRing = kIR, kIMask = kIR - 1u, kIHalf = kIR / 2u;
-  static constexpr uint32_t kPer = kIHalf / 4u / 64u;   // dwords per lane per half
   static_assert(kIHalf >= kIMirror && (kIR & kIMask) == 0u, "a power-of-two ring of two halves, each >= the mirror");
-  static_assert(kIHalf % 256u == 0u, "whole dwords per lane");
   uint8_t* lds;          // kIRing + kIMirror bytes
   const uint8_t* g;      // block start in HBM
   uint32_t csize;
   uint32_t filled;       // input bytes staged so far (multiple of kIHalf)
-  bool pend = false;     // kAhead: the half at `filled` is in flight into nlo/nhi
-  uint32_t nlo[kAhead ? kPer : 1], nhi[kAhead ? kPer : 1];
-
-  // the aligned dwords holding input bytes [at + 4 d, at + 4 d + 4), d = lane + 64 k
-  // (aligned dwords only: each covers a needed byte, so none can fault)
-  __device__ __forceinline__ void load(uint32_t at, uint32_t* lo, uint32_t* hi) const {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t P = at + 4u * (lane + 64u * k);
-      lo[k] = hi[k] = 0u;
-      if (P < csize) {
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + P) & 3u);
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(g + P - mis);
-        lo[k] = a[0];
-        if (mis != 0u && P + 4u - mis < csize) hi[k] = a[1];
-      }
-    }
-  }
-  __device__ __forceinline__ void put(uint32_t at, const uint32_t* lo, const uint32_t* hi) {
-    const uint32_t lane = lane_id();
-    const uint32_t rp = at & kIMask;
-    uint32_t* r32 = reinterpret_cast<uint32_t*>(lds);
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t d = lane + 64u * k;
-      const uint32_t P = at + 4u * d;
-      uint32_t w = 0;
-      if (P < csize) {
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + P) & 3u);
-        w = __builtin_amdgcn_alignbyte(hi[k], lo[k], mis);
-        const uint32_t have = csize - P;
-        if (have < 4u) w &= (1u << (8u * have)) - 1u;
-      }
-      r32[(rp >> 2) + d] = w;
-      if (rp == 0 && d < kIMirror / 4u) r32[kIRing / 4u + d] = w;
-    }
-  }
 
   __device__ void refill() {
-    if constexpr (kAhead) {
-      if (!pend) load(filled, nlo, nhi);
-      put(filled, nlo, nhi);
-      filled += kIHalf;
-      load(filled, nlo, nhi);      // the next half: in flight while this one is decoded
-      pend = true;
-      return;
-    }
     const uint32_t lane = lane_id();
     const uint32_t rp = filled & kIMask;
     uint32_t* r32 = reinterpret_cast<uint32_t*>(lds);
@@ -642,9 +586,9 @@ struct RingWindow {
   }
 };
 
-template <uint32_t kORing, uint32_t kIR, bool kAhead>
-__device__ int decode_ring(InRing<kIR, kAhead>& in, uint8_t* __restrict__ ring, uint8_t* __restrict__ o, int csize,
-                           int osize, int target) {
+template <uint32_t kORing, uint32_t kIR>
+__device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t* __restrict__ o, int csize, int osize,
+                           int target) {
   constexpr uint32_t kOMask = kORing - 1u;
   constexpr uint32_t kIRing = kIR, kIMask = kIR - 1u;
   const uint32_t lane = lane_id();
@@ -986,9 +930,8 @@ __device__ __forceinline__ void ring_decode_loop(
           continue;
         }
       }
-      constexpr bool kAhead = kIR == 8192u && KDB_LZ4_IRING_AHEAD;
-      InRing<kIR, kAhead> in{iring, g, (uint32_t)csize, 0u};
-      const int r = decode_ring<kORing, kIR, kAhead>(in, ring, o, csize, osize, tgt);
+      InRing<kIR> in{iring, g, (uint32_t)csize, 0u};
+      const int r = decode_ring<kORing, kIR>(in, ring, o, csize, osize, tgt);
       if (lane == 0) {
         if (kFrame) {
           ret[v] = r > 0 ? 0 : -1;
