@@ -227,10 +227,12 @@ __device__ __forceinline__ SvcArgs svc_fetch(const SvcBox* box, uint32_t sidx, u
   if (lane < chunks) l4[lane] = c0;
   constexpr uint32_t kMore = (kSvcInBytes / 16u + 63u) / 64u - 1u;
   if (chunks > 64u) {
+    // every load unconditional (indices clamped to the last chunk, inside the
+    // slot): with per-lane conditions around them the compiler kept the array
+    // in scratch memory, a round trip per chunk (ScratchSize 160 per lane)
     uint4 r[kMore];
 #pragma unroll
-    for (uint32_t k = 0; k < kMore; k++)
-      if (lane + 64u * (k + 1u) < chunks) r[k] = in4[lane + 64u * (k + 1u)];
+    for (uint32_t k = 0; k < kMore; k++) r[k] = in4[min(lane + 64u * (k + 1u), chunks - 1u)];
 #pragma unroll
     for (uint32_t k = 0; k < kMore; k++)
       if (lane + 64u * (k + 1u) < chunks) l4[lane + 64u * (k + 1u)] = r[k];
@@ -249,10 +251,10 @@ __device__ __forceinline__ void svc_fetch_input(const SvcBox* box, uint32_t sidx
   const uint4* in4 = reinterpret_cast<const uint4*>(box->slot[sidx].in);
   uint4* l4 = reinterpret_cast<uint4*>(lds);
   constexpr uint32_t kAll = (kSvcInBytes / 16u + 63u) / 64u;
-  uint4 r[kAll];
+  if (chunks == 0u) return;
+  uint4 r[kAll];   // (unconditional loads, clamped: see svc_fetch)
 #pragma unroll
-  for (uint32_t k = 0; k < kAll; k++)
-    if (lane + 64u * k < chunks) r[k] = in4[lane + 64u * k];
+  for (uint32_t k = 0; k < kAll; k++) r[k] = in4[min(lane + 64u * k, chunks - 1u)];
 #pragma unroll
   for (uint32_t k = 0; k < kAll; k++)
     if (lane + 64u * k < chunks) l4[lane + 64u * k] = r[k];
