@@ -135,9 +135,10 @@ class HostPipeline:
         self.frame_off = np.zeros(n + 1, np.uint64)
         self._trace = None        # [(kind, chunk, start Event, end Event)] while profile() runs
         self._pool = []           # events for the traced runs, made before them
+        self._kinds = None        # the span kinds traced (None: all)
 
-    def _mark(self, st) -> "Event | None":
-        if self._trace is None:
+    def _mark(self, st, kind: str = "") -> "Event | None":
+        if self._trace is None or (kind and self._kinds is not None and kind not in self._kinds):
             return None
         # from a pool made before the traced run: creating events inside it
         # delayed the compress loop's enqueues behind its host waits (traced
@@ -147,7 +148,7 @@ class HostPipeline:
         return e
 
     def _span(self, kind: str, c: int, e0, st) -> None:
-        if self._trace is not None:
+        if self._trace is not None and e0 is not None:
             self._trace.append((kind, c, e0, self._mark(st)))
 
     def _range(self, c: int) -> tuple[int, int]:
@@ -169,7 +170,7 @@ class HostPipeline:
             ds = self.dstreams[c % self.cdrain]
             _lib.check(L.kdb_lz4_event_sync(done[c].ptr), "event_sync")
             tot = int(self.h_tot.np[8 * c: 8 * c + 8].view(np.uint64)[0])
-            e0 = self._mark(ds)
+            e0 = self._mark(ds, "d2h")
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_frames.ptr + host_off, self.d_packed.ptr + lo * self.slot,
                                             tot, ds.ptr), "d2h frames")
             self._span("d2h", c, e0, ds)
@@ -185,7 +186,7 @@ class HostPipeline:
             st = self.streams[c % S].ptr
             cm, dm = self.h_cmeta.ptr, self.d_cmeta.ptr
             hs = self.cup if serial else self.streams[c % S]   # the stream of the chunk's host-to-device copies
-            e0 = self._mark(hs)
+            e0 = self._mark(hs, "h2d")
             for base, w in ((0, 8), (8 * n, 4), (12 * n, 8)):
                 _lib.check(L.kdb_lz4_memcpy_h2d(dm + base + w * lo, cm + base + w * lo, w * m, hs.ptr), "h2d meta")
             _lib.check(L.kdb_lz4_memcpy_h2d(self.d_raw.ptr + lo * size, self.h_raw.ptr + lo * size, m * size, hs.ptr),
@@ -194,7 +195,7 @@ class HostPipeline:
             if serial:
                 hdone[c].record(self.cup)
                 _lib.check(L.kdb_lz4_stream_wait_event(st, hdone[c].ptr), "stream_wait_event")
-            e0 = self._mark(self.streams[c % S])
+            e0 = self._mark(self.streams[c % S], "kernel")
             flen = self.d_cres.ptr + 4 * lo
             stat = self.d_cres.ptr + 4 * n + 4 * lo
             _lib.check(L.kdb_lz4_compress_frames_batch(
@@ -259,13 +260,13 @@ class HostPipeline:
             m = hi - lo
             st = self.streams[c % S].ptr
             f0, f1 = int(self.frame_off[lo]), int(self.frame_off[hi])
-            e0 = self._mark(self.streams[c % S])
+            e0 = self._mark(self.streams[c % S], "h2d")
             _lib.check(L.kdb_lz4_memcpy_h2d(self.d_packed.ptr + f0, self.h_frames.ptr + f0, f1 - f0, st), "h2d frames")
             for base, w in ((0, 8), (8 * n, 4)):
                 _lib.check(L.kdb_lz4_memcpy_h2d(self.d_dmeta.ptr + base + w * lo, self.h_dmeta.ptr + base + w * lo,
                                                 w * m, st), "h2d meta")
             self._span("h2d", c, e0, self.streams[c % S])
-            e0 = self._mark(self.streams[c % S])
+            e0 = self._mark(self.streams[c % S], "kernel")
             olen = self.d_dres.ptr + 4 * lo
             stat = self.d_dres.ptr + 4 * n + 4 * lo
             _lib.check(L.kdb_lz4_decompress_frames_batch(
@@ -276,7 +277,7 @@ class HostPipeline:
             kdone[c].record(self.streams[c % S])
             ds = self.dstreams[c % self.ddrain]
             _lib.check(L.kdb_lz4_stream_wait_event(ds.ptr, kdone[c].ptr), "stream_wait_event")
-            e0 = self._mark(ds)
+            e0 = self._mark(ds, "d2h")
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_out.ptr + lo * size, self.d_out.ptr + lo * size, m * size,
                                             ds.ptr), "d2h out")
             self._span("d2h", c, e0, ds)
@@ -303,7 +304,7 @@ class HostPipeline:
             lo, hi = self._range(c)
             m = hi - lo
             f0, f1 = int(self.frame_off[lo]), int(self.frame_off[hi])
-            e0 = self._mark(up)
+            e0 = self._mark(up, "h2d")
             _lib.check(L.kdb_lz4_memcpy_h2d(self.d_packed.ptr + f0, self.h_frames.ptr + f0, f1 - f0, up.ptr), "h2d frames")
             for base, w in ((0, 8), (8 * n, 4)):
                 _lib.check(L.kdb_lz4_memcpy_h2d(self.d_dmeta.ptr + base + w * lo, self.h_dmeta.ptr + base + w * lo,
@@ -312,7 +313,7 @@ class HostPipeline:
             hdone[c].record(up)
             ks = self.streams[c % S]
             _lib.check(L.kdb_lz4_stream_wait_event(ks.ptr, hdone[c].ptr), "stream_wait_event")
-            e0 = self._mark(ks)
+            e0 = self._mark(ks, "kernel")
             _lib.check(L.kdb_lz4_decompress_frames_batch(
                 ks.ptr, self.d_packed.ptr, self.d_dmeta.ptr + 8 * lo, self.d_dmeta.ptr + 8 * n + 4 * lo, m, max_in,
                 size, self.d_out.ptr, self.d_dconst.ptr + 8 * lo, self.d_dconst.ptr + 8 * n + 4 * lo,
@@ -320,7 +321,7 @@ class HostPipeline:
             self._span("kernel", c, e0, ks)
             kdone[c].record(ks)
             _lib.check(L.kdb_lz4_stream_wait_event(down.ptr, kdone[c].ptr), "stream_wait_event")
-            e0 = self._mark(down)
+            e0 = self._mark(down, "d2h")
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_out.ptr + lo * size, self.d_out.ptr + lo * size, m * size,
                                             down.ptr), "d2h out")
             self._span("d2h", c, e0, down)
@@ -350,7 +351,7 @@ class HostPipeline:
             s.sync()
         return time.perf_counter() - t0
 
-    def profile(self) -> dict:
+    def profile(self, kinds=None) -> dict:
         """Where the host-inclusive time goes: one traced compress and one
         traced decompress (HIP events around every chunk's H2D, kernels and
         D2H on its stream), each kind's busy time as the union of its
@@ -368,6 +369,7 @@ class HostPipeline:
         # traced runs are to show the pipeline the timed runs measure
         self.compress()
         self.decompress()
+        self._kinds = set(kinds) if kinds else None
         for phase in ("compress", "decompress"):
             self._pool = [Event() for _ in range(8 * self.nchunks + 8)]
             self._trace = []
@@ -382,6 +384,9 @@ class HostPipeline:
                 iv.setdefault(kind, []).append((base.elapsed_ms(e0), base.elapsed_ms(e1)))
             res = {"wall_ms": round(wall * 1e3, 3)}
             allcopy = []
+            if not iv:
+                out[phase] = res
+                continue
             for kind, ivs in sorted(iv.items()):
                 res[kind + "_busy_ms"] = round(_union(ivs), 3)
                 res[kind + "_sum_ms"] = round(sum(b - a for a, b in ivs), 3)
@@ -396,8 +401,11 @@ class HostPipeline:
         by = {"compress": (raw, float(self.frame_bytes)), "decompress": (float(self.frame_bytes), raw)}
         for phase, (hb, db) in by.items():
             r = out[phase]
-            r["h2d_gbs_while_busy"] = round(hb / (r["h2d_busy_ms"] * 1e-3) / 1e9, 2)
-            r["d2h_gbs_while_busy"] = round(db / (r["d2h_busy_ms"] * 1e-3) / 1e9, 2)
+            if "h2d_busy_ms" in r:
+                r["h2d_gbs_while_busy"] = round(hb / (r["h2d_busy_ms"] * 1e-3) / 1e9, 2)
+            if "d2h_busy_ms" in r:
+                r["d2h_gbs_while_busy"] = round(db / (r["d2h_busy_ms"] * 1e-3) / 1e9, 2)
+        self._kinds = None
         return out
 
     def free(self) -> None:
