@@ -136,6 +136,7 @@ class HostPipeline:
         self._trace = None        # [(kind, chunk, start Event, end Event)] while profile() runs
         self._pool = []           # events for the traced runs, made before them
         self._kinds = None        # the span kinds traced (None: all)
+        self._base = None         # the traced run's time origin
 
     def _mark(self, st, kind: str = "") -> "Event | None":
         if self._trace is None or (kind and self._kinds is not None and kind not in self._kinds):
@@ -186,7 +187,10 @@ class HostPipeline:
             st = self.streams[c % S].ptr
             cm, dm = self.h_cmeta.ptr, self.d_cmeta.ptr
             hs = self.cup if serial else self.streams[c % S]   # the stream of the chunk's host-to-device copies
-            e0 = self._mark(hs, "h2d")
+            # (serial: traced by the hdone events the run records anyway -- event
+            # records between these copies slowed the compress 88.6 -> 96.9 ms,
+            # profiles/r06/r06_k_trace_ab.json)
+            e0 = None if serial else self._mark(hs, "h2d")
             for base, w in ((0, 8), (8 * n, 4), (12 * n, 8)):
                 _lib.check(L.kdb_lz4_memcpy_h2d(dm + base + w * lo, cm + base + w * lo, w * m, hs.ptr), "h2d meta")
             _lib.check(L.kdb_lz4_memcpy_h2d(self.d_raw.ptr + lo * size, self.h_raw.ptr + lo * size, m * size, hs.ptr),
@@ -218,6 +222,11 @@ class HostPipeline:
             drain(c)
         for s in self.streams + self.dstreams + [self.cup]:
             s.sync()
+        if serial and self._trace is not None and (self._kinds is None or "h2d" in self._kinds):
+            # the one copy stream runs its chunks back to back: chunk c's copies
+            # span from the previous chunk's hdone (the trace's base for c = 0)
+            for c in range(self.nchunks):
+                self._trace.append(("h2d", c, hdone[c - 1] if c else self._base, hdone[c]))
         t = time.perf_counter() - t0
         self.frame_bytes = host_off
         flen = self.h_cres.np[: 4 * n].view(np.uint32).astype(np.uint64)
@@ -375,6 +384,7 @@ class HostPipeline:
             self._trace = []
             base = Event()
             base.record(self.streams[0])
+            self._base = base
             for ds in self.dstreams + [self.dup, self.ddown, self.cup]:   # every traced stream starts after the base event
                 _lib.check(lib().kdb_lz4_stream_wait_event(ds.ptr, base.ptr), "stream_wait_event")
             wall = getattr(self, phase)()
