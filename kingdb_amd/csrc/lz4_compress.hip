@@ -34,6 +34,7 @@
 //  * the byte emission of a sequence.
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <type_traits>
 
 #include "lz4_device.h"
@@ -1706,12 +1707,9 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
         "lz4_compress_kernel<true, false, 2u, 1u>"},
        {"lz4_compress_kernel<true, true, 0u, 1u>", "lz4_compress_kernel<true, true, 1u, 1u>",
         "lz4_compress_kernel<true, true, 2u, 1u>"}}};
-  static const char* const names10[2][3] = {
-      {"lz4_compress_kernel<false, true, 0u, 10u>", "lz4_compress_kernel<false, true, 1u, 10u>",
-       "lz4_compress_kernel<false, true, 2u, 10u>"},
-      {"lz4_compress_kernel<true, true, 0u, 10u>", "lz4_compress_kernel<true, true, 1u, 10u>",
-       "lz4_compress_kernel<true, true, 2u, 10u>"}};
-  launch_note(W > 1 ? names10[F][Em] : names[F][Sm][Em]);
+  static const std::string multi = std::string("lz4_compress_kernel<") + (F ? "true" : "false") + ", true, " +
+                                   std::to_string(Em) + "u, " + std::to_string(W) + "u>";
+  launch_note(W > 1 ? multi.c_str() : names[F][Sm][Em]);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * W), lds, st, src, src_off, src_len, n, min_len, in_cap, dst, dst_off,
                      dst_cap, frame_len, ret, work, batch, census, cls, work_queues(in_cap), guide);
   e = hipGetLastError();
@@ -1856,15 +1854,22 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
 #ifndef KDB_LZ4_WG10_DEFAULT
 #define KDB_LZ4_WG10_DEFAULT 1
 #endif
+      // waves per workgroup: 10 (one 160 KiB workgroup per CU) or 5 (two of
+      // 80 KiB: the same 10 per CU), a build-time choice for A/B
+#ifndef KDB_LZ4_CWAVES
+#define KDB_LZ4_CWAVES 10
+#endif
+      constexpr uint32_t CW = KDB_LZ4_CWAVES;
+      static_assert(CW == 5 || CW == 10, "10 per CU: 16 KiB x 5 = 64 steps, x 10 = 128 steps of 1 280 bytes");
       static const bool wg10 = kdb_tune("KDB_LZ4_WG10", KDB_LZ4_WG10_DEFAULT) != 0;
       if (wg10)
-        r = frame ? (bat ? launch_one<true, true, kEmitBatch, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+        r = frame ? (bat ? launch_one<true, true, kEmitBatch, CW>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
                                                                   dst_off, dst_cap, frame_len, ret, census, 0, guide)
-                         : launch_one<true, true, kEmitDirect, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
+                         : launch_one<true, true, kEmitDirect, CW>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
                                                                    dst_off, dst_cap, frame_len, ret, census, 0, guide))
-                  : (bat ? launch_one<false, true, kEmitBatch, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax,
+                  : (bat ? launch_one<false, true, kEmitBatch, CW>(st, lds, src, src_off, src_len, n, 0u, kSmallMax,
                                                                    dst, dst_off, dst_cap, frame_len, ret, census, 0, guide)
-                         : launch_one<false, true, kEmitDirect, 10>(st, lds, src, src_off, src_len, n, 0u, kSmallMax,
+                         : launch_one<false, true, kEmitDirect, CW>(st, lds, src, src_off, src_len, n, 0u, kSmallMax,
                                                                     dst, dst_off, dst_cap, frame_len, ret, census, 0,
                                                                     guide));
       else

@@ -171,15 +171,21 @@ class HostPipeline:
             ds = self.dstreams[c % self.cdrain]
             _lib.check(L.kdb_lz4_event_sync(done[c].ptr), "event_sync")
             tot = int(self.h_tot.np[8 * c: 8 * c + 8].view(np.uint64)[0])
-            e0 = self._mark(ds, "d2h")
+            e0 = None if serial else self._mark(ds, "d2h")
             _lib.check(L.kdb_lz4_memcpy_d2h(self.h_frames.ptr + host_off, self.d_packed.ptr + lo * self.slot,
                                             tot, ds.ptr), "d2h frames")
             self._span("d2h", c, e0, ds)
+            if serial and tracing("d2h"):
+                dend[c] = self._mark(ds)
             chunk_off[c] = host_off
             host_off += tot
 
         serial = self.cserial
         hdone = [Event() for _ in range(self.nchunks)] if serial else None
+        dend = [None] * self.nchunks       # (serial, traced) each frames copy's end
+
+        def tracing(kind: str) -> bool:
+            return self._trace is not None and (self._kinds is None or kind in self._kinds)
         t0 = time.perf_counter()
         for c in range(self.nchunks):
             lo, hi = self._range(c)
@@ -199,7 +205,7 @@ class HostPipeline:
             if serial:
                 hdone[c].record(self.cup)
                 _lib.check(L.kdb_lz4_stream_wait_event(st, hdone[c].ptr), "stream_wait_event")
-            e0 = self._mark(self.streams[c % S], "kernel")
+            e0 = None if serial else self._mark(self.streams[c % S], "kernel")
             flen = self.d_cres.ptr + 4 * lo
             stat = self.d_cres.ptr + 4 * n + 4 * lo
             _lib.check(L.kdb_lz4_compress_frames_batch(
@@ -222,11 +228,24 @@ class HostPipeline:
             drain(c)
         for s in self.streams + self.dstreams + [self.cup]:
             s.sync()
-        if serial and self._trace is not None and (self._kinds is None or "h2d" in self._kinds):
-            # the one copy stream runs its chunks back to back: chunk c's copies
-            # span from the previous chunk's hdone (the trace's base for c = 0)
+        if serial and self._trace is not None:
+            # Serial mode is traced with the events the run records anyway, plus
+            # one at the end of each frames copy: event records between the
+            # copies slowed the compress (88.6 -> 96.9 ms with records around
+            # every H2D span, profiles/r06/r06_k_trace_ab.json).  A span starts
+            # at the latest event its stream had to wait for:
+            #   h2d    (the one copy stream, back to back): the previous chunk's hdone;
+            #   kernel (stream c % S): its chunk's hdone and that stream's previous chunk's done;
+            #   d2h    (dstream c % cdrain): its chunk's done and that stream's previous frames copy.
+            base = self._base
             for c in range(self.nchunks):
-                self._trace.append(("h2d", c, hdone[c - 1] if c else self._base, hdone[c]))
+                if tracing("h2d"):
+                    self._trace.append(("h2d", c, hdone[c - 1] if c else base, hdone[c]))
+                if tracing("kernel"):
+                    self._trace.append(("kernel", c, [hdone[c]] + ([done[c - S]] if c >= S else []), done[c]))
+                if tracing("d2h") and dend[c] is not None:
+                    prev = c - self.cdrain
+                    self._trace.append(("d2h", c, [done[c]] + ([dend[prev]] if prev >= 0 else []), dend[c]))
         t = time.perf_counter() - t0
         self.frame_bytes = host_off
         flen = self.h_cres.np[: 4 * n].view(np.uint32).astype(np.uint64)
@@ -390,7 +409,10 @@ class HostPipeline:
                 _lib.check(lib().kdb_lz4_stream_wait_event(ds.ptr, base.ptr), "stream_wait_event")
             wall = getattr(self, phase)()
             spans, self._trace = self._trace, None
-            return wall, [(kind, base.elapsed_ms(e0), base.elapsed_ms(e1)) for kind, _c, e0, e1 in spans]
+
+            def at(e):   # an event's time, or the latest of several
+                return max(base.elapsed_ms(x) for x in e) if isinstance(e, list) else base.elapsed_ms(e)
+            return wall, [(kind, at(e0), at(e1)) for kind, _c, e0, e1 in spans]
 
         # three traced round trips, as the timed runs alternate the phases; each
         # phase's run of median wall time is reported (the statistic of the timed
