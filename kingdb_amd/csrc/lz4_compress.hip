@@ -1854,13 +1854,15 @@ hipError_t launch_compress(bool frame, hipStream_t st, const uint8_t* src, const
 #ifndef KDB_LZ4_WG10_DEFAULT
 #define KDB_LZ4_WG10_DEFAULT 1
 #endif
-      // waves per workgroup: 10 (one 160 KiB workgroup per CU) or 5 (two of
-      // 80 KiB: the same 10 per CU), a build-time choice for A/B
+      // waves per workgroup: 10 (one 160 KiB workgroup per CU), or 5 for A/B:
+      // two 80 KiB workgroups would make the same 10 per CU by the 1 280-byte
+      // step rule, but the hardware admitted one -- compress 8.0 -> 15.1 ms
+      // (profiles/r06/r06_n_w5.txt)
 #ifndef KDB_LZ4_CWAVES
 #define KDB_LZ4_CWAVES 10
 #endif
       constexpr uint32_t CW = KDB_LZ4_CWAVES;
-      static_assert(CW == 5 || CW == 10, "10 per CU: 16 KiB x 5 = 64 steps, x 10 = 128 steps of 1 280 bytes");
+      static_assert(CW == 5 || CW == 10, "16 KiB regions: 5 or 10 per 160 KiB");
       static const bool wg10 = kdb_tune("KDB_LZ4_WG10", KDB_LZ4_WG10_DEFAULT) != 0;
       if (wg10)
         r = frame ? (bat ? launch_one<true, true, kEmitBatch, CW>(st, lds, src, src_off, src_len, n, 0u, kSmallMax, dst,
