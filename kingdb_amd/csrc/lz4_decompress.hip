@@ -535,26 +535,55 @@ struct InRing {
   uint32_t csize;
   uint32_t filled;       // input bytes staged so far (multiple of kIHalf)
 
+  // One half of the ring: every lane's loads go out before the first is
+  // waited for.  Round 6 had them per dword behind a branch (P < csize, then
+  // the second word when misaligned), which the compiler serialised: 16 HBM
+  // round trips per 4 KiB half, ~1/4 of a 1 MiB part's decode.  Now the
+  // indices are clamped to the block's last aligned dword instead, so every
+  // load is unconditional (and, as before, only dwords holding a block byte
+  // are read, so none can fault); bytes past the block are masked to zero.
+  // (kBatch dwords per lane in flight -- 8 of an 8 KiB ring's 16, 4 of a
+  // 4 KiB ring's 8 -- keeps the ring kernels' VGPRs, and so their waves per
+  // SIMD, where they were: all 16 took the mixed kernel to 169 VGPRs, all 8
+  // the 4 KiB one to 112.)
   __device__ void refill() {
+    constexpr uint32_t kPer = kIHalf / 256u, kBatch = kPer >= 16u ? 8u : kPer / 2u;   // dwords per lane
+    static_assert(kIHalf % 256u == 0u && kPer % kBatch == 0u, "a half is whole batches of every lane's dwords");
     const uint32_t lane = lane_id();
     const uint32_t rp = filled & kIMask;
     uint32_t* r32 = reinterpret_cast<uint32_t*>(lds);
-#pragma unroll 4
-    for (uint32_t d = lane; d < kIHalf / 4u; d += 64u) {
-      const uint32_t P = filled + 4u * d;
-      uint32_t w = 0;
-      if (P < csize) {
-        // aligned dwords only: each covers a needed byte, so none can fault
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + P) & 3u);
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(g + P - mis);
-        const uint32_t lo = a[0];
-        const uint32_t hi = (mis != 0u && P + 4u - mis < csize) ? a[1] : 0u;
-        w = __builtin_amdgcn_alignbyte(hi, lo, mis);
-        const uint32_t have = csize - P;
-        if (have < 4u) w &= (1u << (8u * have)) - 1u;
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3u);   // uniform: filled % 4 == 0
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(g - mis);
+    const uint32_t last = (csize - 1u + mis) >> 2;                          // holds the block's last byte
+#pragma unroll 1
+    for (uint32_t b = 0; b < kPer; b += kBatch) {
+      uint32_t w[kBatch];
+      if (csize == 0u) {
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) w[k] = 0u;
+      } else {
+        uint32_t lo[kBatch], hi[kBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+          const uint32_t i = (filled >> 2) + lane + 64u * (b + k);
+          lo[k] = a[min(i, last)];
+          hi[k] = a[min(i + 1u, last)];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) {
+          const uint32_t P = filled + 4u * (lane + 64u * (b + k));
+          uint32_t x = __builtin_amdgcn_alignbyte(hi[k], lo[k], mis);
+          const uint32_t have = P < csize ? csize - P : 0u;
+          if (have < 4u) x &= (1u << (8u * have)) - 1u;
+          w[k] = x;
+        }
       }
-      r32[(rp >> 2) + d] = w;
-      if (rp == 0 && d < kIMirror / 4u) r32[kIRing / 4u + d] = w;
+#pragma unroll
+      for (uint32_t k = 0; k < kBatch; ++k) {
+        const uint32_t d = lane + 64u * (b + k);
+        r32[(rp >> 2) + d] = w[k];
+        if (rp == 0 && d < kIMirror / 4u) r32[kIRing / 4u + d] = w[k];
+      }
     }
     filled += kIHalf;
   }
