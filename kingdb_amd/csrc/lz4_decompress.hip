@@ -621,6 +621,25 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
   constexpr uint32_t kOMask = kORing - 1u;
   constexpr uint32_t kIRing = kIR, kIMask = kIR - 1u;
   const uint32_t lane = lane_id();
+  // the output ring's byte at position p: LDS address (p mod kORing) | rbase,
+  // one v_and_or -- the ring starts the kernel's dynamic LDS, address 0 (the
+  // ring kernels have no static LDS: checked at launch, ring_kernel_ok), so
+  // its base is a multiple of kORing
+  // (one VALU: the mask in a VGPR, the base in an SGPR -- gfx9's VOP3 reads
+  // one SGPR at most, so the compiler left the two as an and + an or)
+  typedef __attribute__((address_space(3))) uint8_t lds_r8;
+  const uint32_t rbase = lds_addr(ring), vmask = vgpr(kOMask);
+  // the fast path's whole-step ring stores (below): 1 MiB parts decode
+  // 4.97 -> 4.23 ms; the 4 KiB input ring's launch (a mixed batch's 64 KiB
+  // values) measured slower with them (decompress min of 9: 1.86 against
+  // 1.68 ms masked, profiles/r06/r06_v_ab_*.txt), so it keeps the masked ones
+  constexpr bool kWhole = kIR > 4096u;
+  auto ring_at = [&](uint32_t p) -> uint32_t {
+    uint32_t a;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(p), "v"(vmask), "s"(rbase));
+    return a;
+  };
+#define RG(p) (((lds_r8*)(uintptr_t)ring_at((uint32_t)(p)))[0])
   const int iend = unii(csize), oend = unii(osize);
   const int oexit = unii(min(target, oend - (int)kMfLimit));    // lz4.cc:908-910
   const int far_ip = iend - (int)(2 + 1 + kLastLiterals) - 62;   // as in decode_block
@@ -644,10 +663,24 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
       // decode_block's fast path, over the rings, on the vector unit like
       // decode_block's (uniform state in VGPRs): the literal load reads the
       // input ring (its mirror covers the wrap; the loop runs while 512
-      // bytes past ip are staged), stores are masked (ring slots past the
-      // run may still be match sources), and the match source must lie in
-      // the output ring.  A sequence whose next token sits on lane 63 (its
-      // second byte not loaded) ends the loop after it, q to be re-read.
+      // bytes past ip are staged), and the match source must lie in the
+      // output ring, at most kORing - 64 bytes back.  A sequence whose next
+      // token sits on lane 63 (its second byte not loaded) ends the loop
+      // after it, q to be re-read.
+      //
+      // As in decode_block, the ring stores are whole 64-lane steps with no
+      // lane mask (round 6): the bytes past a run land on output not yet
+      // produced, or on ring slots of positions more than kORing - 64 back,
+      // which no match reads from the ring (the fast path's bound above; the
+      // general path reads those from HBM).  The HBM stores stay exact: a
+      // buffer store whose offset is out of range (2^31) for the lanes past
+      // the run, so no exec mask and no 64-bit address per store.  The
+      // match's first step is a plain copy, unconditionally; an overlapping
+      // match rewrites it (its HBM bytes are stored by the rewrite only).
+      const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(o, 0, 0x7fffffff, 0x00020000);
+      auto ost = [&](uint8_t b, bool w, int pos) {
+        __builtin_amdgcn_raw_buffer_store_b8(b, orsrc, w ? pos : (int)0x80000000, 0, 0);
+      };
       const int lim_ip = min(far_ip, (int)in.filled - (int)kIMirror);
       int vip = vgpr(ip), vop = vgpr(op);
       uint32_t vq = vgpr(q);
@@ -674,53 +707,105 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
         const int mx = (mn + 1) >> 4;
         const int xm = e * mx;
         const int mlen = mn + xm + (int)kMinMatch;
-        if (unii((lim_ip - vip) | (far_op - vop) | (45 - xl) | (opl - off) | (254 - xm) | ((int)kORing - off)) < 0)
+        if (unii((lim_ip - vip) | (far_op - vop) | (45 - xl) | (opl - off) | (254 - xm) | ((int)kORing - 64 - off)) < 0)
           break;
-        if ((int)lane < lit) {
-          ring[(uint32_t)(vop + (int)lane) & kOMask] = (uint8_t)v;
-          o[vop + (int)lane] = (uint8_t)v;
-        }
-        const uint32_t nt = (uint32_t)unii(lit + 2 + mx);
-        vq = vgpr(readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8));
-        vip = ls + lit + 2 + mx;
-        header(vq, vip);
-        v = in.lds[((uint32_t)ls & kIMask) + lane];   // the next sequence's literals (in the ring + mirror)
-        const int ref = opl - off;
-        asm volatile("" ::: "memory");
-        const int steps = unii(mlen);
-        if (unii(off - min(mlen, 64)) < 0) {
-          if (unii(off) > 0) {
-            const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
-            const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
-#pragma unroll 1
-            for (int i = 0; i < steps; i += 64) {
-              const int j = i + (int)lane;
-              const uint8_t b = ring[(uint32_t)(ref + i + rr) & kOMask];
-              if (j < mlen) {
-                ring[(uint32_t)(opl + j) & kOMask] = b;
-                o[opl + j] = b;
+        uint32_t nt;
+        if constexpr (kWhole) {
+          RG(vop + (int)lane) = (uint8_t)v;
+          ost((uint8_t)v, (int)lane < lit, vop + (int)lane);
+          nt = (uint32_t)unii(lit + 2 + mx);
+          vq = vgpr(readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8));
+          vip = ls + lit + 2 + mx;
+          header(vq, vip);
+          v = in.lds[((uint32_t)ls & kIMask) + lane];   // the next sequence's literals (in the ring + mirror)
+          const int ref = opl - off;
+          asm volatile("" ::: "memory");
+          const int steps = unii(mlen);
+          const bool overlap = unii(off - min(mlen, 64)) < 0;
+          {
+            const uint8_t b0 = RG(ref + (int)lane);
+            RG(opl + (int)lane) = b0;
+            ost(b0, !overlap && (int)lane < mlen, opl + (int)lane);
+          }
+          asm volatile("" ::: "memory");
+          if (unii((off - min(mlen, 64)) | (64 - mlen)) < 0) {
+            if (overlap) {
+              if (unii(off) > 0) {
+                const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+                const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+  #pragma unroll 1
+                for (int i = 0; i < steps; i += 64) {
+                  const int j = i + (int)lane;
+                  const uint8_t b = RG(ref + i + rr);
+                  RG(opl + j) = b;
+                  ost(b, j < mlen, opl + j);
+                }
+              } else {                              // offset 0: zeros (see decode_block)
+  #pragma unroll 1
+                for (int i = 0; i < steps; i += 64) {
+                  const int j = i + (int)lane;
+                  RG(opl + j) = 0;
+                  ost(0, j < mlen, opl + j);
+                }
               }
-            }
-          } else {                                // offset 0: zeros (see decode_block)
-#pragma unroll 1
-            for (int i = 0; i < steps; i += 64) {
-              const int j = i + (int)lane;
-              if (j < mlen) {
-                ring[(uint32_t)(opl + j) & kOMask] = 0;
-                o[opl + j] = 0;
+            } else {
+  #pragma unroll 1
+              for (int i = 64; i < steps; i += 64) {
+                const int j = i + (int)lane;
+                const uint8_t b = RG(ref + j);
+                RG(opl + j) = b;
+                ost(b, j < mlen, opl + j);
+                asm volatile("" ::: "memory");
               }
             }
           }
         } else {
-#pragma unroll 1
-          for (int i = 0; i < steps; i += 64) {
-            const int j = i + (int)lane;
-            const uint8_t b = ring[(uint32_t)(ref + j) & kOMask];
-            if (j < mlen) {
-              ring[(uint32_t)(opl + j) & kOMask] = b;
-              o[opl + j] = b;
+          if ((int)lane < lit) {
+            RG(vop + (int)lane) = (uint8_t)v;
+            o[vop + (int)lane] = (uint8_t)v;
+          }
+          nt = (uint32_t)unii(lit + 2 + mx);
+          vq = vgpr(readlane(v, nt) | (readlane(v, min(nt + 1u, 63u)) << 8));
+          vip = ls + lit + 2 + mx;
+          header(vq, vip);
+          v = in.lds[((uint32_t)ls & kIMask) + lane];   // the next sequence's literals (in the ring + mirror)
+          const int ref = opl - off;
+          asm volatile("" ::: "memory");
+          const int steps = unii(mlen);
+          if (unii(off - min(mlen, 64)) < 0) {
+            if (unii(off) > 0) {
+              const int r0 = (int)lane - off * (int)((lanef + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+              const int rr = r0 < 0 ? r0 + off : (r0 >= off ? r0 - off : r0);
+  #pragma unroll 1
+              for (int i = 0; i < steps; i += 64) {
+                const int j = i + (int)lane;
+                const uint8_t b = RG(ref + i + rr);
+                if (j < mlen) {
+                  RG(opl + j) = b;
+                  o[opl + j] = b;
+                }
+              }
+            } else {                                // offset 0: zeros (see decode_block)
+  #pragma unroll 1
+              for (int i = 0; i < steps; i += 64) {
+                const int j = i + (int)lane;
+                if (j < mlen) {
+                  RG(opl + j) = 0;
+                  o[opl + j] = 0;
+                }
+              }
             }
-            asm volatile("" ::: "memory");
+          } else {
+  #pragma unroll 1
+            for (int i = 0; i < steps; i += 64) {
+              const int j = i + (int)lane;
+              const uint8_t b = RG(ref + j);
+              if (j < mlen) {
+                RG(opl + j) = b;
+                o[opl + j] = b;
+              }
+              asm volatile("" ::: "memory");
+            }
           }
         }
         asm volatile("" ::: "memory");
@@ -767,7 +852,7 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
         const int j = i + (int)lane;
         const uint8_t b = in.lds[(uint32_t)(ip + done + j) & kIMask];
         if (j < piece) {
-          ring[(uint32_t)(op + done + j) & kOMask] = b;
+          RG(op + done + j) = b;
           o[op + done + j] = b;
         }
       }
@@ -800,9 +885,11 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
     const int mlen = length + (int)kMinMatch;
     if (op + mlen > oend - (int)kLastLiterals) return -ip - 1;    // lz4.cc:1024
     asm volatile("" ::: "memory");
-    if ((uint32_t)off > kORing) {
-      // the source left the ring: read it back from this wave's own output in
-      // HBM (ordered after the stores by a workgroup-scope release/acquire)
+    if ((uint32_t)off > kORing - 64u) {
+      // the source left the ring -- or may have: the fast path's whole-step
+      // stores reach up to 64 bytes past its output into slots of positions
+      // kORing - 63 .. kORing back: read it back from this wave's own output
+      // in HBM (ordered after the stores by a workgroup-scope release/acquire)
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -810,7 +897,7 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
         const int j = i + (int)lane;
         const uint8_t b = j < mlen ? o[ref + j] : (uint8_t)0;
         if (j < mlen) {
-          ring[(uint32_t)(op + j) & kOMask] = b;
+          RG(op + j) = b;
           o[op + j] = b;
         }
         asm volatile("" ::: "memory");
@@ -819,9 +906,9 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
         const int j = i + (int)lane;
-        const uint8_t b = ring[(uint32_t)(ref + j) & kOMask];
+        const uint8_t b = RG(ref + j);
         if (j < mlen) {
-          ring[(uint32_t)(op + j) & kOMask] = b;
+          RG(op + j) = b;
           o[op + j] = b;
         }
         asm volatile("" ::: "memory");
@@ -834,9 +921,9 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
 #pragma unroll 1
       for (int i = 0; i < mlen; i += 64) {
         const int j = i + (int)lane;
-        const uint8_t b = ring[(uint32_t)(ref + i + rr) & kOMask];
+        const uint8_t b = RG(ref + i + rr);
         if (j < mlen) {
-          ring[(uint32_t)(op + j) & kOMask] = b;
+          RG(op + j) = b;
           o[op + j] = b;
         }
       }
@@ -847,7 +934,7 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
       for (int i = 0; i < mlen; i += 64) {
         const int j = i + (int)lane;
         if (j < mlen) {
-          ring[(uint32_t)(op + j) & kOMask] = 0;
+          RG(op + j) = 0;
           o[op + j] = 0;
         }
       }
@@ -856,6 +943,7 @@ __device__ int decode_ring(InRing<kIR>& in, uint8_t* __restrict__ ring, uint8_t*
     op += mlen;
   }
   return op;
+#undef RG
 }
 
 // Values of this launch's class: out size > out_small or block > in_small.
@@ -1109,11 +1197,21 @@ static hipError_t launch_one(hipStream_t st, size_t lds, const uint8_t* src, con
   return e != hipSuccess ? e : r;
 }
 
+// decode_ring addresses its output ring as (p mod kORing) | base: the ring
+// kernels must have no static LDS, so their dynamic LDS (the ring first)
+// starts at address 0.  Checked once per kernel.
+static bool ring_kernel_ok(const void* kern) {
+  hipFuncAttributes a{};
+  return hipFuncGetAttributes(&a, kern) == hipSuccess && a.sharedSizeBytes == 0;
+}
+
 template <bool F, uint32_t R>
 static hipError_t launch_big(hipStream_t st, const uint8_t* src, const uint64_t* src_off, const uint32_t* in_len,
                              uint32_t n, uint32_t in_small, uint32_t out_small, uint8_t* dst, const uint64_t* dst_off,
                              const uint32_t* out_cap, const uint32_t* target, uint32_t* out_len, int32_t* ret) {
   auto kern = lz4_decompress_big_kernel<F, R>;
+  static const bool ok = ring_kernel_ok(reinterpret_cast<const void*>(kern));
+  if (!ok) return hipErrorInvalidDeviceFunction;
   static const uint32_t prio = env_prio();
   const size_t lds = ring_lds<R, 8192u>();
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);
@@ -1162,6 +1260,8 @@ static hipError_t launch_mixed(hipStream_t st, const uint8_t* src, const uint64_
                                const uint64_t* dst_off, const uint32_t* out_cap, const uint32_t* target,
                                uint32_t* out_len, int32_t* ret) {
   auto kern = lz4_decompress_mixed_kernel<F, kIR>;
+  static const bool ok = ring_kernel_ok(reinterpret_cast<const void*>(kern));
+  if (!ok) return hipErrorInvalidDeviceFunction;
   const size_t lds = ring_lds<4096u, kIR>();
   if (decompress_lds_bytes(in_small, out_small) > lds) return hipErrorInvalidValue;   // the small pass's staging
   const uint32_t grid = persistent_grid(reinterpret_cast<const void*>(kern), lds, n);

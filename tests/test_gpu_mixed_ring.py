@@ -94,3 +94,48 @@ def test_mixed_frames_byu16_ring_vs_oracle(orc):
     for x in (dense, doff, tot):
         x.free()
     b.free()
+
+
+def _edge_value(rng, n, dists):
+    """Random bytes with 40-byte copies from `dists` back every ~120 bytes, and
+    periodic runs (offsets 1..63, longer than the offset): the oracle's parse
+    turns them into fast-path sequences whose matches start at those offsets."""
+    x = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    p, k = max(dists) + 64, 0
+    while p + 300 < n:
+        if k % 5 == 4:
+            o = int(rng.integers(1, 64))
+            ln = int(rng.integers(o + 1, o + 140))
+            for i in range(ln):
+                x[p + i] = x[p + i - o]
+            p += ln
+        else:
+            d = dists[k % len(dists)]
+            x[p:p + 40] = x[p - d:p - d + 40]
+            p += 40
+        p += int(rng.integers(20, 61))
+        k += 1
+    return bytes(x)
+
+
+def test_ring_edge_offsets_vs_oracle(gpu, orc):
+    """The ring decoder's fast path (lz4_decompress.hip decode_ring): the 8 KiB
+    input ring's launch (a batch with a 1 MiB part) stores whole 64-lane steps
+    into the 4 KiB output ring, so a match from 4 032 bytes back or more is read
+    from the wave's own output in HBM; the 4 KiB input ring's launch (values of
+    at most 64 KiB) keeps exact stores.  Matches from just inside to just past
+    both edges (4 032 / 4 096 back), and periodic ones, decode to the input;
+    the frames equal the oracle's."""
+    rng = np.random.default_rng(4032)
+    dists = [4000, 4031, 4032, 4033, 4063, 4064, 4065, 4095, 4096, 4097, 5000]
+    big = [_edge_value(rng, 1 << 20, dists), _edge_value(rng, 300000, dists[::-1])]
+    small = [_edge_value(rng, n, dists) for n in (9000, 20000, 65536)]
+    for vals in (big + small, small):
+        want = [orc.frame(v) for v in vals]
+        frames = gpu.compress_frames(vals)
+        assert frames == want
+        back = gpu.decompress_frames(frames, [len(v) for v in vals])
+        assert all(st == 0 and out == v for (st, out), v in zip(back, vals))
+        blocks = [orc.compress(v) for v in vals]
+        dec = gpu.decompress_blocks(blocks, [len(v) for v in vals])
+        assert all(r == len(v) and out == v for (r, out), v in zip(dec, vals))
