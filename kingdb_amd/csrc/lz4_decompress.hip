@@ -510,8 +510,9 @@ __global__ __launch_bounds__(1024) void lz4_decompress_kernel(
 // bytes: KingDB's 1 MB parts, byU32 blocks) or whose block exceeds its staging
 // size.  Same decode rules (lz4.cc:876-1042); the value streams through two
 // LDS rings instead of being staged whole:
-//   * output: a 64 KiB ring -- every match source lies within 65 535 bytes --
-//     with each decoded byte also written straight to its place in HBM;
+//   * output: a 4 KiB ring, each decoded byte also written straight to its
+//     place in HBM; a match from further back than the ring serves (decode_ring:
+//     4 032 bytes) reads its source from there;
 //   * input: an 8 KiB ring refilled 4 KiB at a time from HBM (bytes at and
 //     past the block end staged as 0, like the zeroed tail of the LDS decoder),
 //     plus a 512-byte mirror of its start so the 256-byte register window
