@@ -95,12 +95,13 @@ class Oracle:
         r = self.lib.orc_compress_limited(_ptr(src), _ptr(dst), len(data), cap)
         return None if r == 0 else dst[:r].tobytes()
 
-    def decompress(self, block: bytes, size: int) -> tuple[int, bytes]:
-        """LZ4_decompress_safe_partial(block, dst, len(block), size, size)."""
+    def decompress(self, block: bytes, size: int, target: int | None = None) -> tuple[int, bytes]:
+        """LZ4_decompress_safe_partial(block, dst, len(block), target, size); target defaults to size."""
         src = np.zeros(len(block) + 64, dtype=np.uint8)
         src[: len(block)] = np.frombuffer(block, dtype=np.uint8)
         dst = np.zeros(size + 64, dtype=np.uint8)
-        r = self.lib.orc_decompress_safe_partial(_ptr(src), _ptr(dst), len(block), size, size)
+        r = self.lib.orc_decompress_safe_partial(_ptr(src), _ptr(dst), len(block), size if target is None else target,
+                                                 size)
         return r, (dst[:r].tobytes() if r > 0 else b"")
 
     def frame(self, data: bytes) -> bytes:

@@ -139,3 +139,29 @@ def test_ring_edge_offsets_vs_oracle(gpu, orc):
         blocks = [orc.compress(v) for v in vals]
         dec = gpu.decompress_blocks(blocks, [len(v) for v in vals])
         assert all(r == len(v) and out == v for (r, out), v in zip(dec, vals))
+
+
+def test_ring_partial_decode_vs_oracle(gpu, orc):
+    """LZ4_decompress_safe_partial with a target below the output size through the
+    ring decoder (outputs above the LDS decoder's 8 KiB: decode_ring's oexit =
+    min(target, oend - 12), lz4.cc:908-910): the decode stops after the sequence
+    that reaches the target, on both ring launches; return codes and bytes equal
+    the oracle's, whose partial decode malformed.npz pins to the reference."""
+    rng = np.random.default_rng(908)
+    pool = oracle.g1_pool(orc)
+    big = [bytes(pool[:1 << 20]), bytes(pool[1 << 20:(1 << 20) + 300000])]
+    small = [bytes(pool[o:o + n]) for o, n in ((5000, 9000), (70000, 30000), (200000, 65536))]
+    for vals in (big + small, small):
+        blocks, sizes, targets = [], [], []
+        for v in vals:
+            b = orc.compress(v)
+            for t in (1, 64, 4031, 4097, len(v) // 3, len(v) - 13, len(v) - 1,
+                      int(rng.integers(1, len(v)))):
+                blocks.append(b)
+                sizes.append(len(v))
+                targets.append(int(t))
+        got = gpu.decompress_blocks(blocks, sizes, targets)
+        for i, ((r, out), b, s, t) in enumerate(zip(got, blocks, sizes, targets)):
+            er, eout = orc.decompress(b, s, t)
+            assert r == er, (i, s, t, r, er)
+            assert out == eout, (i, s, t)
