@@ -84,5 +84,31 @@ __device__ __forceinline__ uint32_t step(uint32_t c, uint32_t byte, const uint32
   return s_t[(c ^ byte) & 0xffu] ^ (c >> 8);
 }
 
+// Slice-by-4: t[k][i] is the register after byte i and k zero bytes, so four
+// message bytes (one little-endian dword) take four independent lookups
+// instead of four dependent ones.
+struct Tables4 {
+  uint32_t t[4][256];
+};
+constexpr Tables4 make_tables4() {
+  Tables4 s{};
+  const Tables b = make_tables();
+  for (uint32_t i = 0; i < 256; i++) s.t[0][i] = b.t[i];
+  for (int k = 1; k < 4; k++)
+    for (uint32_t i = 0; i < 256; i++) s.t[k][i] = (s.t[k - 1][i] >> 8) ^ s.t[0][s.t[k - 1][i] & 0xffu];
+  return s;
+}
+static __constant__ Tables4 kTab4 = make_tables4();
+
+// The four 256-entry tables (4 KiB) staged in LDS by the calling block.
+__device__ __forceinline__ void stage_table4(uint32_t* s4) {
+  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) s4[i] = kTab4.t[i >> 8][i & 0xffu];
+}
+// the register after the four bytes of w (byte 0 first)
+__device__ __forceinline__ uint32_t step4(uint32_t c, uint32_t w, const uint32_t* s4) {
+  c ^= w;
+  return s4[768u + (c & 0xffu)] ^ s4[512u + ((c >> 8) & 0xffu)] ^ s4[256u + ((c >> 16) & 0xffu)] ^ s4[c >> 24];
+}
+
 }  // namespace crc
 }  // namespace kdb_lz4
