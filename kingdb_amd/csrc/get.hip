@@ -182,7 +182,52 @@ __global__ __launch_bounds__(kFinishBlock) void get_finish_kernel(
   __syncthreads();
   const uint32_t lane = lane_id();
   const uint32_t nw = gridDim.x * (kFinishBlock / 64);
-  for (uint32_t v = blockIdx.x * (kFinishBlock / 64) + threadIdx.x / 64u; v < n; v += nw) {
+  // 64 values per wave at a time, a lane each (round 6): a value whose status
+  // and length follow from its walk and its one frame's status -- no slide, no
+  // raw tail, no checksum -- is finished by its lane; the wave then takes the
+  // others one by one (below).  One value per wave had every wave wait two
+  // dependent metadata round trips per value: 354 us per 1 Mi values.
+  for (uint32_t c0 = (blockIdx.x * (kFinishBlock / 64) + threadIdx.x / 64u) * 64u; c0 < n; c0 += nw * 64u) {
+    bool other = false;
+    {
+      const uint32_t v = c0 + lane;
+      if (v < n) {
+        const ValueWalk w = walks[v];
+        const uint64_t f0 = frame_first[v];
+        int32_t st = 0;
+        uint64_t defined = 0;
+        bool done = true;
+        if (w.end == kEndCap || f0 + w.nframes > frame_cap) {
+          st = KDB_LZ4_VALUE_UNSUPPORTED;
+        } else if (w.nframes > 1u) {
+          done = false;
+        } else {
+          bool failed = false;
+          if (w.nframes == 1u) {
+            if (f_status[f0] != 0) {
+              failed = true;
+            } else if (f_out[f0] != out_off[v]) {
+              done = false;                 // a slide: the wave's path
+            } else {
+              defined = f_len[f0];
+            }
+          }
+          if (failed || w.end == kEndError) st = -1;
+          else if (w.end == kEndTail) done = w.tail_len == 0;
+          else if (verify) done = false;     // kEndDone with the checksum: the wave's CRC
+        }
+        if (done) {
+          status[v] = st;
+          out_len[v] = defined;
+        }
+        other = !done;
+      }
+    }
+    uint64_t todo = ballot(other);
+#pragma unroll 1
+  while (todo) {
+    const uint32_t v = c0 + (uint32_t)__builtin_ctzll(todo);
+    todo &= todo - 1ull;
     const ValueWalk w = walks[v];
     const uint64_t f0 = frame_first[v];
     const uint8_t* s = stored + stored_off[v];
@@ -230,6 +275,7 @@ __global__ __launch_bounds__(kFinishBlock) void get_finish_kernel(
       status[v] = st;
       out_len[v] = defined;
     }
+  }
   }
 }
 
@@ -280,7 +326,7 @@ hipError_t launch_get_values(hipStream_t st, const uint8_t* stored, const uint64
   e = launch_decompress(true, st, stored, f_off, f_avail, (uint32_t)frame_cap, max_frame_in, max_frame_out, out,
                         f_out, f_raw, nullptr, f_len, f_status);
   if (e != hipSuccess) return e;
-  const uint32_t fg = (n + 3) / 4 < 16384u ? (n + 3) / 4 : 16384u;
+  const uint32_t fg = (n + 255) / 256 < 4096u ? (n + 255) / 256 : 4096u;   // 64 values per wave per pass
   hipLaunchKernelGGL(get_finish_kernel, dim3(fg), dim3(kFinishBlock), 0, st, stored, stored_off, svc, out, out_off, n,
                      frame_first, frame_cap, f_off, f_out, f_raw, f_len, f_status, walks, verify, checksum,
                      checksum_initial, out_len, status);
