@@ -225,57 +225,57 @@ __global__ __launch_bounds__(kFinishBlock) void get_finish_kernel(
     }
     uint64_t todo = ballot(other);
 #pragma unroll 1
-  while (todo) {
-    const uint32_t v = c0 + (uint32_t)__builtin_ctzll(todo);
-    todo &= todo - 1ull;
-    const ValueWalk w = walks[v];
-    const uint64_t f0 = frame_first[v];
-    const uint8_t* s = stored + stored_off[v];
-    uint8_t* o = out + out_off[v];
-    int32_t st = 0;
-    uint64_t defined = 0;
-    if (w.end == kEndCap || f0 + w.nframes > frame_cap) {
-      st = KDB_LZ4_VALUE_UNSUPPORTED;   // more frames than the launch's frame capacity
-    } else {
-      // frames in order: the first failure ends the value; a frame that decoded
-      // fewer bytes than its header announced moves the later ones down
-      bool failed = false;
-      for (uint32_t k = 0; k < w.nframes; k++) {
-        const uint64_t f = f0 + k;
-        if (f_status[f] != 0) { failed = true; break; }
-        const uint64_t at = f_out[f] - out_off[v];
-        const uint32_t got = f_len[f];
-        if (at != defined) {           // slide down (front to back: never overlaps wrongly)
-          for (uint64_t j = 0; j < got; j += 64u) {
-            const uint64_t i = j + lane;
-            const uint8_t b = i < got ? o[at + i] : (uint8_t)0;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (i < got) o[defined + i] = b;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    while (todo) {
+      const uint32_t v = c0 + (uint32_t)__builtin_ctzll(todo);
+      todo &= todo - 1ull;
+      const ValueWalk w = walks[v];
+      const uint64_t f0 = frame_first[v];
+      const uint8_t* s = stored + stored_off[v];
+      uint8_t* o = out + out_off[v];
+      int32_t st = 0;
+      uint64_t defined = 0;
+      if (w.end == kEndCap || f0 + w.nframes > frame_cap) {
+        st = KDB_LZ4_VALUE_UNSUPPORTED;   // more frames than the launch's frame capacity
+      } else {
+        // frames in order: the first failure ends the value; a frame that decoded
+        // fewer bytes than its header announced moves the later ones down
+        bool failed = false;
+        for (uint32_t k = 0; k < w.nframes; k++) {
+          const uint64_t f = f0 + k;
+          if (f_status[f] != 0) { failed = true; break; }
+          const uint64_t at = f_out[f] - out_off[v];
+          const uint32_t got = f_len[f];
+          if (at != defined) {           // slide down (front to back: never overlaps wrongly)
+            for (uint64_t j = 0; j < got; j += 64u) {
+              const uint64_t i = j + lane;
+              const uint8_t b = i < got ? o[at + i] : (uint8_t)0;
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+              if (i < got) o[defined + i] = b;
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
           }
+          defined += got;
         }
-        defined += got;
+        if (failed) {
+          st = -1;
+        } else if (w.end == kEndError) {
+          st = -1;
+        } else if (w.end == kEndTail) {
+          const uint64_t to = defined;          // == walk's tail_out unless a frame decoded short
+          for (uint64_t i = lane; i < w.tail_len; i += 64u) o[to + i] = s[w.tail_in + i];
+          defined += w.tail_len;
+        } else if (verify) {                    // kEndDone: the reference compares the CRC
+          const FrameMsg msg{s, f_off + f0, stored_off[v], w.nframes, verify == 1 ? 2u : 1u, svc[v]};
+          const uint64_t mlen = (verify == 1 ? 2u : 1u) * svc[v];
+          const uint32_t c = crc::extend_wave(checksum_initial[v], mlen, msg, s_t);
+          if (c != checksum[v]) st = -2;
+        }
       }
-      if (failed) {
-        st = -1;
-      } else if (w.end == kEndError) {
-        st = -1;
-      } else if (w.end == kEndTail) {
-        const uint64_t to = defined;          // == walk's tail_out unless a frame decoded short
-        for (uint64_t i = lane; i < w.tail_len; i += 64u) o[to + i] = s[w.tail_in + i];
-        defined += w.tail_len;
-      } else if (verify) {                    // kEndDone: the reference compares the CRC
-        const FrameMsg msg{s, f_off + f0, stored_off[v], w.nframes, verify == 1 ? 2u : 1u, svc[v]};
-        const uint64_t mlen = (verify == 1 ? 2u : 1u) * svc[v];
-        const uint32_t c = crc::extend_wave(checksum_initial[v], mlen, msg, s_t);
-        if (c != checksum[v]) st = -2;
+      if (lane == 0) {
+        status[v] = st;
+        out_len[v] = defined;
       }
     }
-    if (lane == 0) {
-      status[v] = st;
-      out_len[v] = defined;
-    }
-  }
   }
 }
 
